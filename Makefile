@@ -1,0 +1,46 @@
+# Build everything in-tree (the .so files travel to the GPU box with the snapshot).
+#
+#   convolutionalencdec_amd/lib/libviterbi_amd.so        HIP kernels + C ABI (include/viterbi_amd.h)
+#   convolutionalencdec_amd/lib/libviterbi_legacy_k<K>.so legacy C API (include/viterbiDecoder.h,
+#                                                         include/convEncode.h) for code config params/k<K>
+#   oracle/...                                            test-only checker (oracle/Makefile)
+
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+LIB := convolutionalencdec_amd/lib
+CSRC := convolutionalencdec_amd/csrc
+
+HIP_SRCS := $(CSRC)/vtb_api.hip $(CSRC)/vtb_lds_path.hip $(CSRC)/vtb_reg_path.hip
+HIP_HDRS := $(CSRC)/vtb_internal.h include/viterbi_amd.h
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
+
+LEGACY_SRCS := $(CSRC)/legacy/convEncode.c $(CSRC)/legacy/convHelpers.c $(CSRC)/legacy/viterbiDecoder.c
+LEGACY_HDRS := include/viterbiDecoder.h include/viterbiDecoderButterflyk1.h include/convEncode.h include/convHelpers.h
+LEGACY_CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wno-unused-function
+
+LEGACY_KS := 5 7 9
+
+.PHONY: all lib legacy oracle clean
+all: lib legacy oracle
+
+lib: $(LIB)/libviterbi_amd.so
+legacy: $(foreach K,$(LEGACY_KS),$(LIB)/libviterbi_legacy_k$(K).so)
+
+$(LIB)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(LIB)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libviterbi_amd.so: $(patsubst $(CSRC)/%.hip,$(LIB)/obj/%.o,$(HIP_SRCS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(LIB)/libviterbi_legacy_k%.so: $(LEGACY_SRCS) $(LEGACY_HDRS) params/k%/convCodeParams.c $(LIB)/libviterbi_amd.so
+	$(CC) $(LEGACY_CFLAGS) -shared -Iparams/k$* -Iinclude -o $@ $(LEGACY_SRCS) params/k$*/convCodeParams.c \
+		-L$(LIB) -lviterbi_amd -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(LIB)/obj $(LIB)/*.so
+	$(MAKE) -C oracle clean

@@ -1,0 +1,248 @@
+"""Throughput bench for the MI355X Viterbi decoder (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json metric "decoded info Mbit/s, K=7 r=1/2 soft-dec, batch 4096
+frames"): every rank decodes its own batch of 4096 frames x 1024 information bits of
+K=7 {0113, 0171} rate-1/2 code, 8-bit soft input from a BPSK/AWGN channel at SNR -5 dB
+(4 sps), inputs resident in HBM before timing starts.  A step = one decode launch over
+the rank's batch.  Frames are independent, so ranks share nothing on the data path
+(weak scaling, no collective); the only collectives are the timing barrier and the
+max-over-ranks reduction of the elapsed time.
+
+Prints ONE JSON line on rank 0 (the driver's contract), with the roofline of the decode
+kernel (HIP-event time per launch, algorithmic bytes per launch) and the CPU baseline
+(the reference's own decoder, oracle/_ref, timed on this host's cores at N=1).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "decoded info Mbit/s, K=7 r=1/2 soft-dec, batch 4096 frames @1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+K, G = 7, (0o113, 0o171)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
+    ap.add_argument("--frame-bits", type=int, default=1024)
+    ap.add_argument("--hard", action="store_true", help="hard-decision input instead of 8-bit soft")
+    ap.add_argument("--K", type=int, default=7, choices=(5, 7, 9))
+    ap.add_argument("--snr-db", type=float, default=-5.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def shard_seed(rank, base=314):
+    """Each rank regenerates its own shard from (base seed, rank): disjoint, reproducible."""
+    return base + 1000 * rank
+
+
+class Timer:
+    """Barrier + synchronize bracketing; max over ranks (the driver's timing contract)."""
+
+    def __init__(self, world, device_sync, barrier, allreduce_max):
+        self.world, self.sync, self.barrier, self.allreduce_max = world, device_sync, barrier, allreduce_max
+
+    def run(self, step, steps):
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        self.sync()
+        self.barrier()
+        dt = time.perf_counter() - t0
+        return self.allreduce_max(dt)
+
+
+def cpu_baseline(seconds, threads, frame_bits):
+    """Reference decoder (oracle/_ref/libref_k7.so, compiled from the reference sources) on
+    this host: the speedDecode protocol (speedDecode.c:37-116) with the workload's frame
+    length, one independent decoder state per thread.  Falls back to the oracle port."""
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_k7.so")
+    pkt_bytes = frame_bits // 8
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    threads = max(1, min(threads, avail))
+    if os.path.exists(ref):
+        lib = ctypes.CDLL(ref)
+        lib.ref_speed.restype = ctypes.c_double
+        lib.ref_speed.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int]
+        mbps = lib.ref_speed(seconds, threads, pkt_bytes)
+        return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
+                "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
+                          f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "
+                          f"{seconds:g} s, one decoder state per thread"}
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from helpers import Oracle  # test infrastructure: the checker, used here only as the timed CPU leg
+
+    from convolutionalencdec_amd import synth
+
+    orc = Oracle()
+    frames = 512
+    unc, q = synth.make_frames(K, G, frames, frame_bits, soft=True, seed=7)
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds:
+        orc.decode(K, G, q, frame_bits, soft=True, threads=threads)
+        n += frames
+    dt = time.perf_counter() - t0
+    return {"value": round(n * frame_bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
+            "sample": f"oracle soft decoder (C restatement), {frames} frames x {frame_bits} bits repeated for "
+                      f"{seconds:g} s on {threads} threads"}
+
+
+def load_traffic(workload_key):
+    """HBM bytes per launch measured by the rocprofv3 --pmc passes (profiles/pmc_traffic.json)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_env()
+    import torch
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a ROCm GPU")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+        def barrier():
+            dist.barrier()
+
+        def allreduce_max(x):
+            t = torch.tensor([x], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+    else:
+        def barrier():
+            pass
+
+        def allreduce_max(x):
+            return x
+
+    from convolutionalencdec_amd import ConvCode, ViterbiDecoder, synth
+
+    code = (K, G) if args.K == 7 else (args.K, {5: (0o23, 0o35), 9: (0o561, 0o753)}[args.K])
+    soft = not args.hard
+    F, L = args.frames, args.frame_bits
+    T = L + code[0] - 1
+    unc, rx = synth.make_frames(code[0], code[1], F, L, soft=soft, snr_db=args.snr_db, p=0.0559, seed=shard_seed(rank))
+    dec = ViterbiDecoder(ConvCode(*code), frame_bits=L, soft=soft, device=local)
+    x = torch.from_numpy(rx.reshape(F, -1)).to(dev)
+    out = torch.empty((F, (L + 7) // 8), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        dec.decode_device(x, out=out, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    decoded = out.cpu().numpy()
+    ber = float(np.unpackbits(decoded ^ unc).mean())
+
+    timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
+    elapsed = timer.run(step, args.steps)
+
+    # Per-launch device time with HIP events on the launch stream (roofline numerator).
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bits = F * L * world
+    value = total_bits / (elapsed / args.steps) / 1e6
+    in_b = (2 if soft else 1) * T
+    alg_bytes = F * (in_b + (L + 7) // 8)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    workload_key = f"K{code[0]}_{'soft' if soft else 'hard'}_F{F}_L{L}"
+    traffic = load_traffic(workload_key)
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    cpu = None
+    if world == 1 and args.cpu_seconds > 0 and code[0] == 7:
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads, L)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbit/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"K={code[0]} r=1/2 {'8-bit soft' if soft else 'hard'}-decision Viterbi, {F} frames x {L} "
+                        f"info bits per GPU, AWGN SNR {args.snr_db:g} dB" if soft else
+                        f"K={code[0]} r=1/2 hard-decision Viterbi, {F} frames x {L} info bits per GPU, BSC p=0.0559",
+            "frames_per_gpu": F,
+            "frame_bits": L,
+            "global_batch_frames": F * world,
+            "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
+            "decoded_ber": ber,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 3),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6),
+            "traffic": traffic,
+            "kernel_ms": round(kern_ms, 5),
+            "algorithmic_bytes_per_launch": alg_bytes,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

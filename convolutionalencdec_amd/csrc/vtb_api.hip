@@ -1,0 +1,319 @@
+// C-ABI implementation of include/viterbi_amd.h: code tables, plans, kernel choice,
+// host/device entry points and the multi-GPU shard driver.
+//
+// Host-side only; the trellis work happens in the kernels of vtb_reg_path.hip (fast
+// register-resident path) and vtb_lds_path.hip (baseline path, every K).
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "viterbi_amd.h"
+#include "vtb_internal.h"
+
+#define VTB_VERSION_STRING "viterbi_amd 0.1 (gfx950)"
+
+struct vtb_plan {
+    vtb_code_t code;
+    vtb_input_t input;
+    int32_t L;
+    int32_t T;
+    int device;
+    uint8_t symm[1 << (vtb::kMaxS - 1)];
+    // host-path staging (grown on demand)
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    size_t cap_frames = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int parity(uint64_t x) { return __builtin_popcountll(x) & 1; }
+
+// src/convEncode.c:163-174: reverse the K low bits.
+uint64_t reverse_bits(uint64_t v, int bits) {
+    uint64_t r = 0;
+    for (int i = 0; i < bits; i++) {
+        r = (r << 1) | (v & 1u);
+        v >>= 1;
+    }
+    return r;
+}
+
+int check_code(const vtb_code_t* c) {
+    if (!c) return VTB_ERR_INVALID;
+    if (c->coded_bits != 2) return VTB_ERR_UNSUPPORTED;
+    if (c->constraint_length < VTB_MIN_K || c->constraint_length > VTB_MAX_K) return VTB_ERR_UNSUPPORTED;
+    for (int i = 0; i < 2; i++) {
+        if (c->generators[i] >> c->constraint_length) return VTB_ERR_INVALID;  // taps beyond the constraint length
+        // viterbiDecoder.c:17-25: the symmetric butterfly needs both end taps.
+        if (!((c->generators[i] >> (c->constraint_length - 1)) & 1u) || !(c->generators[i] & 1u)) return VTB_ERR_CODE;
+    }
+    return VTB_OK;
+}
+
+void edge_table(const vtb_code_t* c, uint8_t* symm) {
+    uint64_t p0 = reverse_bits(c->generators[0], c->constraint_length), p1 = reverse_bits(c->generators[1], c->constraint_length);
+    int half = 1 << (c->constraint_length - 2);
+    for (int i = 0; i < half; i++) {
+        uint64_t tapped = uint64_t(i) << 1;  // tappedDelay = i, shift in input 0
+        symm[i] = uint8_t(parity(tapped & p0) | (parity(tapped & p1) << 1));
+    }
+}
+
+size_t in_bytes(const vtb_code_t* c, vtb_input_t in, int32_t L) {
+    size_t T = size_t(L) + size_t(c->constraint_length - 1);
+    return in == VTB_INPUT_SOFT8 ? 2 * T : T;
+}
+
+size_t out_bytes(int32_t L) { return (size_t(L) + 7) / 8; }
+
+bool env_flag_is(const char* name, const char* value) {
+    const char* v = std::getenv(name);
+    return v && std::strcmp(v, value) == 0;
+}
+
+// Which kernel family a plan uses: the register path when it supports the shape, else
+// the LDS path.  VTB_KERNEL=lds|reg forces one (testing / A-B measurement).
+int launch(const vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
+           size_t frames, hipStream_t stream) {
+    vtb::Launch a;
+    a.S = p->code.constraint_length - 1;
+    a.soft = p->input == VTB_INPUT_SOFT8;
+    a.T = p->T;
+    a.L = p->L;
+    a.in = d_in;
+    a.in_stride = in_stride;
+    a.out = d_out;
+    a.out_stride = out_stride;
+    a.frames = frames;
+    a.stream = stream;
+    std::memcpy(a.symm, p->symm, sizeof(a.symm));
+    const bool force_lds = env_flag_is("VTB_KERNEL", "lds");
+    const bool force_reg = env_flag_is("VTB_KERNEL", "reg");
+    hipError_t e;
+    if (!force_lds && vtb::reg_path_supported(a)) {
+        e = vtb::launch_reg_path(a);
+    } else if (!force_reg && vtb::lds_path_supported(a)) {
+        e = vtb::launch_lds_path(a);
+    } else {
+        return VTB_ERR_UNSUPPORTED;
+    }
+    return e == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+bool device_is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vtb_version(void) { return VTB_VERSION_STRING; }
+
+const char* vtb_strerror(int err) {
+    switch (err) {
+        case VTB_OK: return "ok";
+        case VTB_ERR_INVALID: return "invalid argument";
+        case VTB_ERR_CODE: return "generator does not tap both the newest and the oldest input (no butterfly symmetry)";
+        case VTB_ERR_UNSUPPORTED: return "unsupported code or frame length";
+        case VTB_ERR_DEVICE: return "no usable gfx950 device or HIP runtime error";
+        case VTB_ERR_NOMEM: return "out of memory";
+        default: return "unknown error";
+    }
+}
+
+int vtb_code_check(const vtb_code_t* code) { return check_code(code); }
+
+int vtb_edge_table(const vtb_code_t* code, uint8_t* symm) {
+    int e = check_code(code);
+    if (e == VTB_ERR_CODE) e = VTB_OK;  // the table itself exists for any code
+    if (e != VTB_OK) return e;
+    if (!symm) return VTB_ERR_INVALID;
+    edge_table(code, symm);
+    return VTB_OK;
+}
+
+size_t vtb_input_bytes_per_frame(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits) {
+    if (!code || frame_bits < 1 || code->constraint_length < VTB_MIN_K || code->constraint_length > VTB_MAX_K) return 0;
+    return in_bytes(code, input, frame_bits);
+}
+
+size_t vtb_output_bytes_per_frame(int32_t frame_bits) { return frame_bits < 1 ? 0 : out_bytes(frame_bits); }
+
+int vtb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int d = 0; d < n; d++) good += device_is_gfx950(d) ? 1 : 0;
+    return good;
+}
+
+int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, int device) {
+    if (!plan) return VTB_ERR_INVALID;
+    *plan = nullptr;
+    int e = check_code(code);
+    if (e != VTB_OK) return e;
+    if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
+    if (frame_bits < 1) return VTB_ERR_INVALID;
+    if (frame_bits > VTB_MAX_FRAME_BITS) return VTB_ERR_UNSUPPORTED;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return VTB_ERR_DEVICE;
+    if (!device_is_gfx950(device)) return VTB_ERR_DEVICE;
+    vtb_plan* p = new (std::nothrow) vtb_plan();
+    if (!p) return VTB_ERR_NOMEM;
+    p->code = *code;
+    p->input = input;
+    p->L = frame_bits;
+    p->T = frame_bits + code->constraint_length - 1;
+    p->device = device;
+    edge_table(code, p->symm);
+    // Shape check up front so a plan that exists can always launch.
+    vtb::Launch a;
+    a.S = code->constraint_length - 1;
+    a.soft = input == VTB_INPUT_SOFT8;
+    a.T = p->T;
+    a.L = p->L;
+    if (!vtb::reg_path_supported(a) && !vtb::lds_path_supported(a)) {
+        delete p;
+        return VTB_ERR_UNSUPPORTED;
+    }
+    *plan = p;
+    return VTB_OK;
+}
+
+void vtb_plan_destroy(vtb_plan_t* plan) {
+    if (!plan) return;
+    DeviceGuard g(plan->device);
+    if (plan->d_in) (void)hipFree(plan->d_in);
+    if (plan->d_out) (void)hipFree(plan->d_out);
+    if (plan->stream) (void)hipStreamDestroy(plan->stream);
+    delete plan;
+}
+
+int vtb_decode_device(vtb_plan_t* plan, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
+                      size_t frames, void* stream) {
+    if (!plan) return VTB_ERR_INVALID;
+    if (frames == 0) return VTB_OK;
+    if (!d_in || !d_out) return VTB_ERR_INVALID;
+    if (in_stride < in_bytes(&plan->code, plan->input, plan->L) || out_stride < out_bytes(plan->L))
+        return VTB_ERR_INVALID;
+    DeviceGuard g(plan->device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    return launch(plan, d_in, in_stride, d_out, out_stride, frames, static_cast<hipStream_t>(stream));
+}
+
+int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_t frames) {
+    if (!plan) return VTB_ERR_INVALID;
+    if (frames == 0) return VTB_OK;
+    if (!h_in || !h_out) return VTB_ERR_INVALID;
+    DeviceGuard g(plan->device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    const size_t ib = in_bytes(&plan->code, plan->input, plan->L), ob = out_bytes(plan->L);
+    if (!plan->stream && hipStreamCreateWithFlags(&plan->stream, hipStreamNonBlocking) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    if (frames > plan->cap_frames) {
+        if (plan->d_in) (void)hipFree(plan->d_in);
+        if (plan->d_out) (void)hipFree(plan->d_out);
+        plan->d_in = plan->d_out = nullptr;
+        plan->cap_frames = 0;
+        if (hipMalloc(&plan->d_in, frames * ib) != hipSuccess) return VTB_ERR_NOMEM;
+        if (hipMalloc(&plan->d_out, frames * ob) != hipSuccess) return VTB_ERR_NOMEM;
+        plan->cap_frames = frames;
+    }
+    if (hipMemcpyAsync(plan->d_in, h_in, frames * ib, hipMemcpyHostToDevice, plan->stream) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    int e = launch(plan, plan->d_in, ib, plan->d_out, ob, frames, plan->stream);
+    if (e != VTB_OK) return e;
+    if (hipMemcpyAsync(h_out, plan->d_out, frames * ob, hipMemcpyDeviceToHost, plan->stream) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    return hipStreamSynchronize(plan->stream) == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
+}
+
+int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,
+                          uint8_t* h_out, size_t frames, uint32_t device_mask) {
+    int e = check_code(code);
+    if (e != VTB_OK) return e;
+    if (frame_bits < 1) return VTB_ERR_INVALID;
+    if (frames == 0) return VTB_OK;
+    if (!h_in || !h_out) return VTB_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return VTB_ERR_DEVICE;
+    std::vector<int> devs;
+    for (int d = 0; d < ndev && d < 32; d++)
+        if ((device_mask == 0 || ((device_mask >> d) & 1u)) && device_is_gfx950(d)) devs.push_back(d);
+    if (devs.empty()) return VTB_ERR_DEVICE;
+    const size_t ib = in_bytes(code, input, frame_bits), ob = out_bytes(frame_bits);
+    const size_t G = devs.size();
+    std::vector<int> rc(G, VTB_OK);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < G; i++) {
+        // Contiguous shard [i*F/G, (i+1)*F/G): frames are independent, no collective.
+        size_t lo = frames * i / G, hi = frames * (i + 1) / G;
+        th.emplace_back([&, i, lo, hi]() {
+            if (hi <= lo) return;
+            vtb_plan_t* p = nullptr;
+            int r = vtb_plan_create(&p, code, input, frame_bits, devs[i]);
+            if (r == VTB_OK) r = vtb_decode_host(p, h_in + lo * ib, h_out + lo * ob, hi - lo);
+            vtb_plan_destroy(p);
+            rc[i] = r;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r != VTB_OK) return r;
+    return VTB_OK;
+}
+
+int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out) {
+    if (!code || !coded || !out) return VTB_ERR_INVALID;
+    int e = check_code(code);
+    if (e != VTB_OK) return e;
+    const int32_t L = segments - (code->constraint_length - 1);
+    if (L < 1) return VTB_ERR_INVALID;
+    // One cached plan per host thread (the reference API is reentrant per state struct).
+    struct Cache {
+        vtb_plan_t* plan = nullptr;
+        ~Cache() { vtb_plan_destroy(plan); }
+    };
+    thread_local Cache cache;
+    vtb_plan_t*& p = cache.plan;
+    if (!p || p->code.constraint_length != code->constraint_length || p->code.generators[0] != code->generators[0] || p->code.generators[1] != code->generators[1] || p->L != L) {
+        vtb_plan_destroy(p);
+        p = nullptr;
+        int dev = 0;
+        if (const char* s = std::getenv("VTB_LEGACY_DEVICE")) dev = std::atoi(s);
+        int r = vtb_plan_create(&p, code, VTB_INPUT_HARD, L, dev);
+        if (r != VTB_OK) {
+            p = nullptr;
+            return r;
+        }
+    }
+    int r = vtb_decode_host(p, coded, out, 1);
+    if (r != VTB_OK) return r;
+    return (L - 1) / 8 + 1;  // src/viterbiDecoderButterflyk1.c:256
+}
+
+}  // extern "C"

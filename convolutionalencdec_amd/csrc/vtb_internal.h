@@ -1,0 +1,36 @@
+// Internal interface between the C-ABI layer (vtb_api.hip) and the kernel TUs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace vtb {
+
+constexpr int kMaxS = 8;  // K <= 9
+
+// Wave-uniform description of one batch launch.  symm[] is the trellis table of
+// viterbiInitButterflyk1 (reference viterbiDecoderButterflyk1.c:24-29).
+struct Launch {
+    int S = 0;         // state bits, K-1
+    int soft = 0;      // 0: hard byte-per-segment input, 1: 8-bit soft pairs
+    int T = 0;         // trellis steps per frame = L + S
+    int L = 0;         // information bits per frame
+    const uint8_t* in = nullptr;
+    size_t in_stride = 0;
+    uint8_t* out = nullptr;
+    size_t out_stride = 0;
+    size_t frames = 0;
+    hipStream_t stream = nullptr;
+    uint8_t symm[1 << (kMaxS - 1)] = {};
+};
+
+// Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
+// shape limits are reported through *_supported() beforehand.
+bool lds_path_supported(const Launch& a);
+hipError_t launch_lds_path(const Launch& a);
+
+bool reg_path_supported(const Launch& a);
+hipError_t launch_reg_path(const Launch& a);
+
+}  // namespace vtb

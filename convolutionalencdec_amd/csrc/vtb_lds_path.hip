@@ -1,0 +1,228 @@
+// Baseline gfx950 decoder: "LDS path".
+//
+// One wave64 decodes F = 64/G frames; each frame's N = 2^S trellis states are spread over
+// G = min(N, 64) lanes with R = N/G states per lane in registers (state s lives in lane
+// s % G, register s / G).  Per trellis step every lane gathers the two predecessor
+// metrics of each of its states with ds_bpermute (predecessors of s are s>>1 and
+// (s>>1) + N/2, reference viterbiDecoderButterflyk1.c:101-152), does the add-compare-
+// select, and the wave's __ballot of the decisions (one 64-bit word per register per
+// step) is written to LDS.  After the last step the traceback (reference :200-256) walks
+// the LDS survivor words from state 0.
+//
+// This is the simple, obviously-correct kernel: the register-resident kernel
+// (vtb_reg_path.hip) is the fast path; this one also covers every K in 3..9.
+//
+// Metric arithmetic (DESIGN.md "Metric formulation"): centred integer metrics.  For
+// butterfly j with trellis label c = symm[j] and received pair (q0, q1) (hard: bits,
+// Q = 1; soft: bytes, Q = 255) the reference branch metric e = sum_i (c_i ? Q-q_i : q_i)
+// and its complement nQ-e (:104-115) become +mu / -mu with mu = e - Q, computed as one
+// v_dot2_i32_i16.  Subtracting the per-step constant Q from every candidate and working in
+// int32 leaves every comparison -- hence every decision -- unchanged, and int32 never
+// wraps, so no renormalisation is needed (the reference's uint8 renormalisation, :159-183,
+// never wraps either; DESIGN.md proves both).
+
+#include "vtb_internal.h"
+
+namespace vtb {
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ int shfl_idx(int v, int src_lane) {
+    return __builtin_amdgcn_ds_bpermute(src_lane << 2, v);
+}
+
+// Decisions for state s at step t:  bit (fi*G + s%G) of word [t][s/G].
+template <int S>
+struct Geometry {
+    static constexpr int N = 1 << S;
+    static constexpr int G = N < 64 ? N : 64;  // lanes per frame
+    static constexpr int R = N / G;            // states per lane
+    static constexpr int F = 64 / G;           // frames per wave
+};
+
+template <int S, bool SOFT>
+__global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                                        uint8_t* __restrict__ out, size_t out_stride,
+                                                                        int T, int L, size_t frames, int waves_per_block,
+                                                                        Launch table) {
+    using Gm = Geometry<S>;
+    constexpr int N = Gm::N, G = Gm::G, R = Gm::R, F = Gm::F;
+    constexpr int Q = SOFT ? 255 : 1;
+    constexpr int INIT = int(uint8_t(N + 1)) * Q;  // (uint8_t)(NUM_STATES+1), reference :62
+    constexpr int BYTES_PER_SEG = SOFT ? 2 : 1;
+
+    extern __shared__ uint64_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int fi = lane / G;
+    const int lam = lane % G;
+
+    const size_t dec_words = (size_t)T * R;
+    const size_t in_bytes = ((size_t)F * T * BYTES_PER_SEG + 7) & ~size_t(7);
+    uint64_t* dec = smem + (size_t)wave * (dec_words + in_bytes / 8);
+    uint8_t* inbuf = reinterpret_cast<uint8_t*>(dec + dec_words);
+
+    const size_t frame0 = ((size_t)blockIdx.x * waves_per_block + wave) * F;
+    const size_t myframe = frame0 + fi;
+    const bool valid = myframe < frames;
+
+    // Stage this wave's input frames into LDS (coalesced byte loads).
+    const int seg_bytes = T * BYTES_PER_SEG;
+    for (int idx = lane; idx < F * seg_bytes; idx += 64) {
+        int f = idx / seg_bytes, off = idx - f * seg_bytes;
+        uint8_t v = 0;
+        if (frame0 + f < frames) v = in[(frame0 + f) * in_stride + off];
+        inbuf[idx] = v;
+    }
+
+    // Per-register branch-metric coefficients.  Destination d = r*G + lam has
+    // predecessors j = d>>1 and j + N/2; with b = d&1 the candidate from j is m[j] + mu_b
+    // and from j + N/2 is m[j+N/2] - mu_b, where mu_0 = mu(c) and mu_1 = -mu(c).
+    int sig[R], kap[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        int d = r * G + lam;
+        int c = table.symm[d >> 1];
+        int sb = (d & 1) ? -1 : 1;
+        int s0 = ((c & 1) ? -1 : 1) * sb, s1 = ((c & 2) ? -1 : 1) * sb;
+        sig[r] = (s0 & 0xffff) | (s1 << 16);
+        kap[r] = (((c & 1) + ((c >> 1) & 1)) - 1) * Q * sb;
+    }
+
+    int m[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) m[r] = (r * G + lam == 0) ? 0 : INIT;
+
+    __syncthreads();
+
+    const uint8_t* myin = inbuf + fi * seg_bytes;
+    const int src_base = fi * G;
+    for (int t = 0; t < T; t++) {
+        int qp;
+        if (SOFT) {
+            qp = int(myin[2 * t]) | (int(myin[2 * t + 1]) << 16);
+        } else {
+            int c = myin[t];
+            qp = (c & 1) | (((c >> 1) & 1) << 16);
+        }
+        int nm[R];
+        uint64_t ballots[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int lane0 = src_base + (r & 1) * (G / 2) + (lam >> 1);
+            int a0, a1;
+            if (R == 1) {
+                a0 = shfl_idx(m[0], lane0);
+                a1 = shfl_idx(m[0], lane0 + G / 2);
+            } else {
+                a0 = shfl_idx(m[r >> 1], lane0);
+                a1 = shfl_idx(m[(r >> 1) + R / 2], lane0);
+            }
+            typedef short short2_t __attribute__((ext_vector_type(2)));
+            int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, sig[r]), __builtin_bit_cast(short2_t, qp),
+                                            kap[r], false);
+            int c0 = a0 + mu, c1 = a1 - mu;
+            bool d = c0 > c1;  // strict: ties keep the lower predecessor (reference :129-130)
+            nm[r] = d ? c1 : c0;
+            ballots[r] = __ballot(d);
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) m[r] = nm[r];
+        if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < R; r++) dec[(size_t)t * R + r] = ballots[r];
+        }
+    }
+
+    __syncthreads();
+    if (!valid) return;
+
+    // Terminated traceback from state 0 (reference :200-256).
+    auto decision = [&](int t, unsigned s) -> unsigned {
+        uint64_t w = dec[(size_t)t * R + (s / G)];
+        return unsigned(w >> (fi * G + (s % G))) & 1u;
+    };
+    unsigned s = 0;
+    for (int i = 0; i < S; i++) s = (s >> 1) | (decision(T - 1 - i, s) << (S - 1));
+    uint8_t* o = out + myframe * out_stride;
+    unsigned byte = 0;
+    for (int t = L - 1; t >= 0; t--) {
+        byte = ((byte >> 1) | ((s & 1u) << 7)) & 0xffu;
+        if ((t & 7) == 0 && lam == 0) o[t >> 3] = uint8_t(byte);
+        s = (s >> 1) | (decision(t, s) << (S - 1));
+    }
+}
+
+template <int S>
+size_t lds_bytes_per_wave(int soft, int T) {
+    using Gm = Geometry<S>;
+    size_t dec = (size_t)T * Gm::R * 8;
+    size_t inb = ((size_t)Gm::F * T * (soft ? 2 : 1) + 7) & ~size_t(7);
+    return dec + inb;
+}
+
+size_t bytes_per_wave(int S, int soft, int T) {
+    switch (S) {
+        case 2: return lds_bytes_per_wave<2>(soft, T);
+        case 3: return lds_bytes_per_wave<3>(soft, T);
+        case 4: return lds_bytes_per_wave<4>(soft, T);
+        case 5: return lds_bytes_per_wave<5>(soft, T);
+        case 6: return lds_bytes_per_wave<6>(soft, T);
+        case 7: return lds_bytes_per_wave<7>(soft, T);
+        case 8: return lds_bytes_per_wave<8>(soft, T);
+        default: return 0;
+    }
+}
+
+constexpr size_t kLdsLimit = 160 * 1024;
+
+template <int S, bool SOFT>
+hipError_t launch_typed(const Launch& a) {
+    using Gm = Geometry<S>;
+    size_t per_wave = lds_bytes_per_wave<S>(SOFT, a.T);
+    int wpb = int(kLdsLimit / per_wave);
+    if (wpb > kWavesPerBlock) wpb = kWavesPerBlock;
+    if (wpb < 1) return hipErrorInvalidValue;
+    size_t frames_per_block = (size_t)wpb * Gm::F;
+    size_t blocks = (a.frames + frames_per_block - 1) / frames_per_block;
+    size_t lds = per_wave * wpb;
+    auto kern = lds_path_kernel<S, SOFT>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(unsigned(blocks)), dim3(64 * wpb), lds, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, a.frames, wpb, a);
+    return hipGetLastError();
+}
+
+template <bool SOFT>
+hipError_t launch_soft(const Launch& a) {
+    switch (a.S) {
+        case 2: return launch_typed<2, SOFT>(a);
+        case 3: return launch_typed<3, SOFT>(a);
+        case 4: return launch_typed<4, SOFT>(a);
+        case 5: return launch_typed<5, SOFT>(a);
+        case 6: return launch_typed<6, SOFT>(a);
+        case 7: return launch_typed<7, SOFT>(a);
+        case 8: return launch_typed<8, SOFT>(a);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+bool lds_path_supported(const Launch& a) {
+    if (a.S < 2 || a.S > kMaxS || a.T <= a.S) return false;
+    size_t w = bytes_per_wave(a.S, a.soft, a.T);
+    return w > 0 && w <= kLdsLimit;
+}
+
+hipError_t launch_lds_path(const Launch& a) {
+    if (a.frames == 0) return hipSuccess;
+    return a.soft ? launch_soft<true>(a) : launch_soft<false>(a);
+}
+
+}  // namespace vtb

@@ -1,0 +1,112 @@
+"""ctypes binding of the C ABI in include/viterbi_amd.h (libviterbi_amd.so, built in-tree).
+
+Plumbing only: every decode runs in the HIP kernels behind the C ABI.  There is no CPU
+fallback -- if the library is missing or the device is not a gfx950, calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libviterbi_amd.so")
+
+VTB_OK = 0
+VTB_ERR_INVALID = -1
+VTB_ERR_CODE = -2
+VTB_ERR_UNSUPPORTED = -3
+VTB_ERR_DEVICE = -4
+VTB_ERR_NOMEM = -5
+
+VTB_INPUT_HARD = 0
+VTB_INPUT_SOFT8 = 1
+
+# Every symbol include/viterbi_amd.h declares (tests/test_abi.py checks the header and the
+# library against this list).
+EXPORTED_SYMBOLS = (
+    "vtb_version",
+    "vtb_strerror",
+    "vtb_code_check",
+    "vtb_edge_table",
+    "vtb_input_bytes_per_frame",
+    "vtb_output_bytes_per_frame",
+    "vtb_plan_create",
+    "vtb_plan_destroy",
+    "vtb_decode_device",
+    "vtb_decode_host",
+    "vtb_decode_host_multi",
+    "vtb_decode_frame_legacy",
+    "vtb_device_count",
+)
+
+
+class VtbCode(ctypes.Structure):
+    _fields_ = [
+        ("constraint_length", ctypes.c_int32),
+        ("coded_bits", ctypes.c_int32),
+        ("generators", ctypes.c_uint64 * 2),
+    ]
+
+    @classmethod
+    def make(cls, K, g):
+        c = cls()
+        c.constraint_length = int(K)
+        c.coded_bits = 2
+        c.generators[0] = int(g[0])
+        c.generators[1] = int(g[1])
+        return c
+
+
+class VtbError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+
+
+_lib = None
+
+
+def lib():
+    """Load libviterbi_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i32, cp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(VtbCode)
+    L.vtb_version.restype = ctypes.c_char_p
+    L.vtb_version.argtypes = []
+    L.vtb_strerror.restype = ctypes.c_char_p
+    L.vtb_strerror.argtypes = [ctypes.c_int]
+    L.vtb_code_check.argtypes = [cp]
+    L.vtb_edge_table.argtypes = [cp, vp]
+    L.vtb_input_bytes_per_frame.restype = sz
+    L.vtb_input_bytes_per_frame.argtypes = [cp, ctypes.c_int, i32]
+    L.vtb_output_bytes_per_frame.restype = sz
+    L.vtb_output_bytes_per_frame.argtypes = [i32]
+    L.vtb_plan_create.argtypes = [ctypes.POINTER(vp), cp, ctypes.c_int, i32, ctypes.c_int]
+    L.vtb_plan_destroy.restype = None
+    L.vtb_plan_destroy.argtypes = [vp]
+    L.vtb_decode_device.argtypes = [vp, vp, sz, vp, sz, sz, vp]
+    L.vtb_decode_host.argtypes = [vp, vp, vp, sz]
+    L.vtb_decode_host_multi.argtypes = [cp, ctypes.c_int, i32, vp, vp, sz, ctypes.c_uint32]
+    L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
+    L.vtb_device_count.argtypes = []
+    for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
+                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_device_count"):
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def strerror(code):
+    try:
+        return lib().vtb_strerror(int(code)).decode()
+    except Exception:  # pragma: no cover - used while formatting another error
+        return "error"
+
+
+def check(rc, what):
+    if rc < 0:
+        raise VtbError(rc, what)
+    return rc

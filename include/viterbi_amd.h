@@ -1,0 +1,121 @@
+/*
+ * viterbi_amd.h -- C ABI of the MI355X (gfx950) batch Viterbi decoder.
+ *
+ * This is the drop-in boundary for the reference's hot path (SURVEY.md §8 b).  Plain C
+ * types only: pointers, sizes, ints; a HIP stream travels as `void*`.  Everything is
+ * runtime-parameterised (constraint length, generators, frame length, hard/soft), unlike
+ * the reference, which fixes the code at compile time (src/defaultParams/convCodeParams.h).
+ *
+ * Reference interfaces each entry point replaces:
+ *   vtb_code_check          viterbiConfigCheck            src/viterbiDecoder.c:9-30
+ *                           (returns an error code instead of exit(1))
+ *   vtb_edge_table          viterbiInitButterflyk1        src/viterbiDecoderButterflyk1.c:8-44
+ *   vtb_decode_device /     viterbiDecoderHardButterflyk1 src/viterbiDecoderButterflyk1.c:82-263
+ *   vtb_decode_host /       (one terminated frame per call with last=true, batched here
+ *   vtb_decode_host_multi    over many frames; hard input is the reference byte-per-segment
+ *                            layout; soft input is the build-defined 8-bit extension)
+ *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
+ *                           behind include/viterbiDecoder.h (VITERBI_DECODER_HARD)
+ *
+ * Data layout (frame-major, reference layout per frame):
+ *   hard input   T = L + K - 1 bytes per frame, byte t = coded segment t, bit i = output of
+ *                generator g[i] (src/convEncode.c:153-159); only the low 2 bits are read
+ *   soft input   2*T bytes per frame, byte 2t+i = q in [0,255] for coded bit i of segment t
+ *                (0 = confident 0, 255 = confident 1; hard slice is q >= 128)
+ *   output       ceil(L/8) bytes per frame, information bits MSB-first, last byte
+ *                zero-padded (src/viterbiDecoderButterflyk1.c:226-249)
+ *
+ * Decisions are bit-exact with the reference C decoder for hard input (strict '>'
+ * tie-break toward the lower predecessor, (uint8)(N+1) initial metric, full terminated
+ * traceback from state 0).  Soft decisions follow DESIGN.md "Soft-decision format"; soft
+ * input restricted to q in {0,255} reproduces the hard decoder bit for bit.
+ *
+ * Error convention: every function returns 0 (VTB_OK) or a negative VTB_ERR_* code; no
+ * function prints or exits.  Thread-safety: plans are independent; one plan may be used
+ * by one host thread at a time.
+ */
+#ifndef VITERBI_AMD_H
+#define VITERBI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VTB_OK 0
+#define VTB_ERR_INVALID (-1)     /* bad argument (null pointer, L < 1, stride too small ...) */
+#define VTB_ERR_CODE (-2)        /* generator violates the symmetric-butterfly precondition */
+#define VTB_ERR_UNSUPPORTED (-3) /* K, n or frame length outside what the kernels handle */
+#define VTB_ERR_DEVICE (-4)      /* no usable gfx950 device, or a HIP runtime error */
+#define VTB_ERR_NOMEM (-5)       /* host or device allocation failed */
+
+#define VTB_MIN_K 3
+#define VTB_MAX_K 9
+#define VTB_MAX_FRAME_BITS 16384 /* MAX_PKT_LEN_UNCODED_BITS, src/viterbiDecoder.h:18 */
+
+typedef enum { VTB_INPUT_HARD = 0, VTB_INPUT_SOFT8 = 1 } vtb_input_t;
+
+/* A rate-1/n, k=1 convolutional code (Proakis conventions, src/defaultParams/).  Field
+ * names avoid the legacy config macros K, k, n, S so this header can be included next to
+ * convCodeParams.h. */
+typedef struct {
+    int32_t constraint_length; /* K, VTB_MIN_K..VTB_MAX_K */
+    int32_t coded_bits;        /* n, coded bits per segment; must be 2 */
+    uint64_t generators[2];    /* g[], Proakis octal (MSB = newest input), e.g. {0113, 0171} */
+} vtb_code_t;
+
+typedef struct vtb_plan vtb_plan_t;
+
+/* Library version string and a message for a VTB_ERR_* code. */
+const char* vtb_version(void);
+const char* vtb_strerror(int err);
+
+/* 0 if the code is decodable by the symmetric butterfly (every g has its MSB and LSB set),
+ * VTB_ERR_CODE if not, VTB_ERR_UNSUPPORTED / VTB_ERR_INVALID for bad K / n. */
+int vtb_code_check(const vtb_code_t* code);
+
+/* symm[i] = coded segment on the edge state i -> state 2i, i < 2^(K-2). */
+int vtb_edge_table(const vtb_code_t* code, uint8_t* symm);
+
+/* Bytes per frame in each layout (0 for invalid arguments). */
+size_t vtb_input_bytes_per_frame(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits);
+size_t vtb_output_bytes_per_frame(int32_t frame_bits);
+
+/* A plan binds a code, an input format, a frame length L (information bits) and a device
+ * ordinal; it owns the device-side tables and any workspace. */
+int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input, int32_t frame_bits,
+                    int device);
+void vtb_plan_destroy(vtb_plan_t* plan);
+
+/* Decode `frames` frames already resident in device memory, asynchronously on `stream`
+ * (a hipStream_t; NULL = default stream).  d_in: frames * in_stride bytes; d_out: frames *
+ * out_stride bytes.  Strides >= the per-frame sizes above. */
+int vtb_decode_device(vtb_plan_t* plan, const uint8_t* d_in, size_t in_stride, uint8_t* d_out,
+                      size_t out_stride, size_t frames, void* stream);
+
+/* Host buffers (packed, stride = per-frame size): copy in, decode, copy out, synchronise.
+ * Uses the plan's device. */
+int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_t frames);
+
+/* Host buffers sharded across the GPUs in device_mask (bit d = device d; 0 = all visible
+ * devices): contiguous frame ranges, one host thread and stream per device, no
+ * inter-device traffic (frames are independent). */
+int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,
+                          uint8_t* h_out, size_t frames, uint32_t device_mask);
+
+/* One hard-input frame of `segments` coded segments from host memory (the legacy
+ * VITERBI_DECODER_HARD contract).  Returns the reference's byte count
+ * ((segments-K)/8 + 1) on success, or a negative VTB_ERR_* code.  Uses a per-thread
+ * cached plan on device 0 (or $VTB_LEGACY_DEVICE). */
+int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out);
+
+/* Number of gfx950 devices visible (0 if none); negative VTB_ERR_DEVICE on runtime error. */
+int vtb_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

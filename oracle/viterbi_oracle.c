@@ -1,0 +1,322 @@
+/*
+ * TEST INFRASTRUCTURE ONLY -- NOT PART OF THE PRODUCT.  See viterbi_oracle.h.
+ *
+ * Plain-C restatement of the reference algorithm, written from its behaviour (each
+ * function cites the reference file:line it follows).  Kept deliberately simple and
+ * scalar: it is the checker, not the thing measured.
+ */
+#include "viterbi_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORACLE_MAX_S 12
+
+static int parity64(uint64_t x) { return __builtin_popcountll(x) & 1; }
+
+/* convEncode.c:163-174 -- reverse the K low bits (Proakis MSB = newest input -> LSB). */
+static uint64_t reverse_bits(uint64_t v, int bits) {
+    uint64_t r = 0;
+    for (int i = 0; i < bits; i++) {
+        r = (r << 1) | (v & 1u);
+        v >>= 1;
+    }
+    return r;
+}
+
+/* convEncode.c:132-161 -- output bit j = parity(tappedDelay & rev(g[j])), g[0] in the LSB. */
+static uint8_t enc_output(uint64_t tapped, const uint64_t polys[2]) {
+    return (uint8_t)(parity64(tapped & polys[0]) | (parity64(tapped & polys[1]) << 1));
+}
+
+int oracle_config_check(int K, const uint64_t g[2]) {
+    for (int i = 0; i < 2; i++) {
+        if (!((g[i] >> (K - 1)) & 1u) || !(g[i] & 1u)) return i + 1; /* viterbiDecoder.c:20-23 */
+    }
+    return 0;
+}
+
+void oracle_edge_table(int K, const uint64_t g[2], uint8_t* symm) {
+    uint64_t polys[2] = {reverse_bits(g[0], K), reverse_bits(g[1], K)};
+    int half = 1 << (K - 2);
+    for (int i = 0; i < half; i++) {
+        /* tappedDelay = i, then convEncOneInput shifts in a 0 (convEncode.c:19-44). */
+        symm[i] = enc_output(((uint64_t)i) << 1, polys);
+    }
+}
+
+int oracle_encode(int K, const uint64_t g[2], const uint8_t* uncoded, int nbytes, uint8_t* coded) {
+    uint64_t polys[2] = {reverse_bits(g[0], K), reverse_bits(g[1], K)};
+    uint64_t mask = (K >= 64) ? ~0ull : ((1ull << K) - 1);
+    uint64_t reg = 0; /* STARTING_STATE (convEncode.c:6-11) */
+    int out = 0;
+    for (int b = 0; b < nbytes; b++) {
+        for (int i = 7; i >= 0; i--) { /* MSB first (convEncode.c:76-89) */
+            reg = ((reg << 1) | ((uncoded[b] >> i) & 1u)) & mask;
+            coded[out++] = enc_output(reg, polys);
+        }
+    }
+    for (int i = 0; i < K - 1; i++) { /* S zero-tail segments (convEncode.c:100-115) */
+        reg = (reg << 1) & mask;
+        coded[out++] = enc_output(reg, polys);
+    }
+    return out;
+}
+
+/* viterbiDecoderButterflyk1.c:200-256 -- terminated traceback from state 0, skip S tail
+ * decisions, pack the info bits MSB-first. dec is T rows of N bytes. */
+static int traceback(int S, const uint8_t* dec, int T, uint8_t* out) {
+    int N = 1 << S;
+    if (T <= S) return -1;
+    unsigned s = 0;
+    for (int i = 0; i < S; i++) {
+        int t = T - 1 - i;
+        s = (s >> 1) | ((unsigned)dec[(size_t)t * N + s] << (S - 1));
+    }
+    int L = T - S;
+    out[(L - 1) / 8] = 0; /* :226-227 */
+    for (int t = L - 1; t >= 0; t--) {
+        out[t / 8] = (uint8_t)((out[t / 8] >> 1) | ((s & 1u) << 7));
+        s = (s >> 1) | ((unsigned)dec[(size_t)t * N + s] << (S - 1));
+    }
+    return (L - 1) / 8 + 1; /* :256 */
+}
+
+int oracle_decode_hard(int K, const uint64_t g[2], const uint8_t* coded, int T, uint8_t* out) {
+    int S = K - 1, N = 1 << S, half = N / 2;
+    if (S < 1 || S > ORACLE_MAX_S || T <= S) return -1;
+    uint8_t symm[1 << ORACLE_MAX_S];
+    oracle_edge_table(K, g, symm);
+    uint8_t m[1 << ORACLE_MAX_S], nm[1 << ORACLE_MAX_S];
+    uint8_t* dec = (uint8_t*)malloc((size_t)T * N);
+    if (!dec) return -1;
+    m[0] = 0; /* viterbiDecoderButterflyk1.c:59 */
+    for (int i = 1; i < N; i++) m[i] = (uint8_t)(N + 1); /* :62-67, deliberately truncated */
+    unsigned renorm = 0;
+    for (int t = 0; t < T; t++) {
+        uint8_t c = coded[t] & 3u; /* calcHammingDist reads the low n bits (viterbiDecoder.c:278-281) */
+        uint8_t* d = dec + (size_t)t * N;
+        for (int b = 0; b < half; b++) {
+            uint8_t e = (uint8_t)__builtin_popcount((symm[b] ^ c) & 3u); /* :104 */
+            uint8_t ec = (uint8_t)(2 - e);                              /* :107 */
+            uint8_t a0 = (uint8_t)(m[b] + e), a1 = (uint8_t)(m[half + b] + ec);
+            uint8_t b0 = (uint8_t)(m[b] + ec), b1 = (uint8_t)(m[half + b] + e);
+            uint8_t ad = a0 > a1, bd = b0 > b1; /* strict '>' (:129-130) */
+            nm[2 * b] = ad ? a1 : a0;
+            nm[2 * b + 1] = bd ? b1 : b0;
+            d[2 * b] = ad;
+            d[2 * b + 1] = bd;
+        }
+        if (renorm >= 120) { /* :159-183 */
+            uint8_t mn = nm[0];
+            for (int i = 1; i < N; i++)
+                if (nm[i] < mn) mn = nm[i];
+            for (int i = 0; i < N; i++) nm[i] = (uint8_t)(nm[i] - mn);
+            renorm = 0;
+        } else {
+            renorm++;
+        }
+        memcpy(m, nm, (size_t)N);
+    }
+    int r = traceback(S, dec, T, out);
+    free(dec);
+    return r;
+}
+
+int oracle_decode_soft(int K, const uint64_t g[2], const uint8_t* q, int T, uint8_t* out) {
+    int S = K - 1, N = 1 << S, half = N / 2;
+    if (S < 1 || S > ORACLE_MAX_S || T <= S) return -1;
+    uint8_t symm[1 << ORACLE_MAX_S];
+    oracle_edge_table(K, g, symm);
+    int32_t m[1 << ORACLE_MAX_S], nm[1 << ORACLE_MAX_S];
+    uint8_t* dec = (uint8_t*)malloc((size_t)T * N);
+    if (!dec) return -1;
+    m[0] = 0;
+    for (int i = 1; i < N; i++) m[i] = (int32_t)(uint8_t)(N + 1) * 255;
+    for (int t = 0; t < T; t++) {
+        int q0 = q[2 * t], q1 = q[2 * t + 1];
+        uint8_t* d = dec + (size_t)t * N;
+        for (int b = 0; b < half; b++) {
+            int e = ((symm[b] & 1u) ? 255 - q0 : q0) + ((symm[b] & 2u) ? 255 - q1 : q1);
+            int ec = 510 - e;
+            int32_t a0 = m[b] + e, a1 = m[half + b] + ec;
+            int32_t b0 = m[b] + ec, b1 = m[half + b] + e;
+            uint8_t ad = a0 > a1, bd = b0 > b1;
+            nm[2 * b] = ad ? a1 : a0;
+            nm[2 * b + 1] = bd ? b1 : b0;
+            d[2 * b] = ad;
+            d[2 * b + 1] = bd;
+        }
+        memcpy(m, nm, sizeof(int32_t) * (size_t)N);
+    }
+    int r = traceback(S, dec, T, out);
+    free(dec);
+    return r;
+}
+
+typedef struct {
+    int K, soft, T;
+    const uint64_t* g;
+    const uint8_t* in;
+    size_t in_stride;
+    uint8_t* out;
+    size_t out_stride;
+    size_t lo, hi;
+    int err;
+} batch_job_t;
+
+static void* batch_worker(void* arg) {
+    batch_job_t* j = (batch_job_t*)arg;
+    for (size_t f = j->lo; f < j->hi; f++) {
+        const uint8_t* in = j->in + f * j->in_stride;
+        uint8_t* out = j->out + f * j->out_stride;
+        int r = j->soft ? oracle_decode_soft(j->K, j->g, in, j->T, out)
+                        : oracle_decode_hard(j->K, j->g, in, j->T, out);
+        if (r < 0) j->err = 1;
+    }
+    return NULL;
+}
+
+int oracle_decode_batch(int K, const uint64_t g[2], int soft, const uint8_t* in, size_t in_stride,
+                        int T, uint8_t* out, size_t out_stride, size_t frames, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    batch_job_t jobs[64];
+    size_t per = (frames + (size_t)nthreads - 1) / (size_t)nthreads;
+    int started = 0;
+    for (int i = 0; i < nthreads; i++) {
+        size_t lo = (size_t)i * per, hi = lo + per;
+        if (lo >= frames) break;
+        if (hi > frames) hi = frames;
+        jobs[i] = (batch_job_t){K, soft, T, g, in, in_stride, out, out_stride, lo, hi, 0};
+        if (pthread_create(&th[i], NULL, batch_worker, &jobs[i]) != 0) {
+            batch_worker(&jobs[i]);
+            th[i] = 0;
+        }
+        started++;
+    }
+    int err = 0;
+    for (int i = 0; i < started; i++) {
+        if (th[i]) pthread_join(th[i], NULL);
+        err |= jobs[i].err;
+    }
+    return err ? -1 : 0;
+}
+
+/* ---- streaming (reference state machine, viterbiHardState_t viterbiDecoder.h:103-146) ---- */
+#define ORACLE_MAX_SEGMENTS (16384 + ORACLE_MAX_S)
+
+struct oracle_stream {
+    int K, S, N;
+    uint8_t symm[1 << ORACLE_MAX_S];
+    uint8_t m[1 << ORACLE_MAX_S];
+    unsigned iteration, renorm;
+    uint8_t* dec;
+};
+
+oracle_stream_t* oracle_stream_create(int K, const uint64_t g[2]) {
+    if (K < 2 || K - 1 > ORACLE_MAX_S) return NULL;
+    oracle_stream_t* st = (oracle_stream_t*)calloc(1, sizeof(*st));
+    if (!st) return NULL;
+    st->K = K;
+    st->S = K - 1;
+    st->N = 1 << st->S;
+    st->dec = (uint8_t*)malloc((size_t)ORACLE_MAX_SEGMENTS * st->N);
+    if (!st->dec) {
+        free(st);
+        return NULL;
+    }
+    oracle_edge_table(K, g, st->symm);
+    oracle_stream_reset(st);
+    return st;
+}
+
+void oracle_stream_destroy(oracle_stream_t* st) {
+    if (!st) return;
+    free(st->dec);
+    free(st);
+}
+
+void oracle_stream_reset(oracle_stream_t* st) { /* viterbiDecoderButterflyk1.c:46-80 */
+    st->m[0] = 0;
+    for (int i = 1; i < st->N; i++) st->m[i] = (uint8_t)(st->N + 1);
+    st->iteration = 0;
+    st->renorm = 0;
+}
+
+int oracle_stream_decode(oracle_stream_t* st, const uint8_t* coded, int segments, uint8_t* out,
+                         int last, uint8_t* metrics_after) {
+    int N = st->N, half = N / 2, S = st->S;
+    uint8_t nm[1 << ORACLE_MAX_S];
+    for (int i = 0; i < segments; i++) {
+        if (st->iteration >= ORACLE_MAX_SEGMENTS) return -1;
+        uint8_t c = coded[i] & 3u;
+        uint8_t* d = st->dec + (size_t)st->iteration * N;
+        for (int b = 0; b < half; b++) {
+            uint8_t e = (uint8_t)__builtin_popcount((st->symm[b] ^ c) & 3u);
+            uint8_t ec = (uint8_t)(2 - e);
+            uint8_t a0 = (uint8_t)(st->m[b] + e), a1 = (uint8_t)(st->m[half + b] + ec);
+            uint8_t b0 = (uint8_t)(st->m[b] + ec), b1 = (uint8_t)(st->m[half + b] + e);
+            uint8_t ad = a0 > a1, bd = b0 > b1;
+            nm[2 * b] = ad ? a1 : a0;
+            nm[2 * b + 1] = bd ? b1 : b0;
+            d[2 * b] = ad;
+            d[2 * b + 1] = bd;
+        }
+        if (st->renorm >= 120) {
+            uint8_t mn = nm[0];
+            for (int j = 1; j < N; j++)
+                if (nm[j] < mn) mn = nm[j];
+            for (int j = 0; j < N; j++) nm[j] = (uint8_t)(nm[j] - mn);
+            st->renorm = 0;
+        } else {
+            st->renorm++;
+        }
+        memcpy(st->m, nm, (size_t)N);
+        st->iteration++;
+    }
+    if (metrics_after) memcpy(metrics_after, st->m, (size_t)N);
+    int r = 0;
+    if (last) {
+        r = traceback(S, st->dec, (int)st->iteration, out);
+        oracle_stream_reset(st);
+    }
+    return r;
+}
+
+long oracle_bertest_stream(int K, const uint64_t g[2], unsigned seed, int nconfigs, const double* p,
+                           int npkts, int pkt_bytes, uint8_t* uncoded, uint8_t* corrupted) {
+    int T = 8 * pkt_bytes + K - 1;
+    uint8_t* coded = (uint8_t*)malloc((size_t)T);
+    if (!coded) return -1;
+    long flips = 0;
+    srand(seed); /* berTestK7.c:66 */
+    for (int c = 0; c < nconfigs; c++) {
+        for (int k = 0; k < npkts; k++) {
+            uint8_t* u = uncoded + ((size_t)c * npkts + k) * pkt_bytes;
+            uint8_t* x = corrupted + ((size_t)c * npkts + k) * T;
+            for (int j = 0; j < pkt_bytes; j++) u[j] = (uint8_t)rand(); /* :135-138 */
+            oracle_encode(K, g, u, pkt_bytes, coded);                  /* :142 */
+            for (int i = 0; i < T; i++) {                               /* :29-43 */
+                uint8_t corrupt = 0;
+                for (int j = 0; j < 2; j++) {
+                    double fr = (double)rand() / RAND_MAX;
+                    uint8_t flip = fr > p[c] ? 0 : 1;
+                    corrupt = (uint8_t)((corrupt << 1) | flip);
+                    flips += flip;
+                }
+                x[i] = coded[i] ^ corrupt;
+            }
+        }
+    }
+    free(coded);
+    return flips;
+}
+
+long oracle_bit_errors(const uint8_t* a, const uint8_t* b, size_t len) {
+    long e = 0;
+    for (size_t i = 0; i < len; i++) e += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return e;
+}

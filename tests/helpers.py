@@ -1,0 +1,181 @@
+"""Test-side utilities: the oracle binding (test infrastructure only), golden fixtures and
+seeded synthetic frames."""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE_LIB = os.path.join(REPO, "oracle", "build", "liboracle.so")
+REF_DIR = os.path.join(REPO, "oracle", "_ref")
+
+CODES = {5: (0o23, 0o35), 7: (0o113, 0o171), 9: (0o561, 0o753)}
+BERTEST_P = (5.585640e-02, 3.716174e-02, 2.262231e-02)  # berTestK7.c:96
+BERTEST_ERRORS = (92418, 9655, 655)  # reference run, SURVEY.md §4
+
+
+def vp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Oracle:
+    """ctypes view of oracle/build/liboracle.so (the CPU restatement; checker only)."""
+
+    def __init__(self, path=ORACLE_LIB):
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "oracle"], check=True, capture_output=True)
+        L = ctypes.CDLL(path)
+        v, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.oracle_config_check.argtypes = [i, v]
+        L.oracle_edge_table.argtypes = [i, v, v]
+        L.oracle_encode.argtypes = [i, v, v, i, v]
+        L.oracle_decode_hard.argtypes = [i, v, v, i, v]
+        L.oracle_decode_soft.argtypes = [i, v, v, i, v]
+        L.oracle_decode_batch.argtypes = [i, v, i, v, sz, i, v, sz, sz, i]
+        L.oracle_stream_create.restype = v
+        L.oracle_stream_create.argtypes = [i, v]
+        L.oracle_stream_destroy.argtypes = [v]
+        L.oracle_stream_decode.argtypes = [v, v, i, v, i, v]
+        L.oracle_bertest_stream.restype = ctypes.c_long
+        L.oracle_bertest_stream.argtypes = [i, v, ctypes.c_uint, i, v, i, i, v, v]
+        self.L = L
+
+    @staticmethod
+    def _g(g):
+        return (ctypes.c_uint64 * 2)(*g)
+
+    def config_check(self, K, g):
+        return self.L.oracle_config_check(K, self._g(g))
+
+    def edge_table(self, K, g):
+        out = np.zeros(1 << (K - 2), np.uint8)
+        self.L.oracle_edge_table(K, self._g(g), vp(out))
+        return out
+
+    def encode(self, K, g, uncoded):
+        unc = np.ascontiguousarray(uncoded, np.uint8)
+        F, nb = unc.shape
+        T = 8 * nb + K - 1
+        out = np.zeros((F, T), np.uint8)
+        G = self._g(g)
+        for f in range(F):
+            row = np.ascontiguousarray(unc[f])
+            o = np.zeros(T, np.uint8)
+            assert self.L.oracle_encode(K, G, vp(row), nb, vp(o)) == T
+            out[f] = o
+        return out
+
+    def decode(self, K, g, frames, L, soft=False, threads=8):
+        x = np.ascontiguousarray(frames, np.uint8)
+        F = x.shape[0]
+        x = x.reshape(F, -1)
+        T = L + K - 1
+        assert x.shape[1] == (2 * T if soft else T)
+        ob = (L + 7) // 8
+        out = np.zeros((F, ob), np.uint8)
+        rc = self.L.oracle_decode_batch(K, self._g(g), int(soft), vp(x), x.shape[1], T, vp(out), ob, F, threads)
+        assert rc == 0
+        return out
+
+    def stream(self, K, g):
+        return OracleStream(self, K, g)
+
+    def bertest(self, K=7, g=CODES[7], seed=9865, p=BERTEST_P, npkts=10000, pkt_bytes=256):
+        T = 8 * pkt_bytes + K - 1
+        unc = np.zeros((len(p), npkts, pkt_bytes), np.uint8)
+        rx = np.zeros((len(p), npkts, T), np.uint8)
+        pa = (ctypes.c_double * len(p))(*p)
+        flips = self.L.oracle_bertest_stream(K, self._g(g), seed, len(p), pa, npkts, pkt_bytes, vp(unc), vp(rx))
+        return unc, rx, flips
+
+
+class OracleStream:
+    def __init__(self, orc, K, g):
+        self.orc, self.K, self.N = orc, K, 1 << (K - 1)
+        self.h = orc.L.oracle_stream_create(K, orc._g(g))
+
+    def decode(self, coded, out, last):
+        c = np.ascontiguousarray(coded, np.uint8)
+        met = np.zeros(self.N, np.uint8)
+        r = self.orc.L.oracle_stream_decode(self.h, vp(c), len(c), vp(out), int(last), vp(met))
+        return r, met
+
+    def __del__(self):
+        try:
+            self.orc.L.oracle_stream_destroy(self.h)
+        except Exception:
+            pass
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "MANIFEST.json")) as fh:
+        return json.load(fh)
+
+
+def golden_sets(K):
+    """Yield (key, L, uncoded, rx, decoded) for every hard set of constraint length K."""
+    z = load_golden(f"k{K}_hard.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in z})
+    for key in keys:
+        L = int(key.split("_")[0][1:])
+        yield key, L, z[key + "_uncoded"], z[key + "_rx"], z[key + "_decoded"]
+
+
+def random_frames(orc, K, L, frames, p, seed, soft=False, sigma=None, g=None):
+    """Seeded terminated frames through a BSC (hard) or BPSK-AWGN + 8-bit quantiser (soft).
+
+    Soft quantiser: y = (1-2b) + sigma*noise, q = clamp(round((1-y)/2*255)).
+    Returns (uncoded_bytes [F, ceil(L/8)], rx [F, T] or [F, T, 2])."""
+    rng = np.random.default_rng(seed)
+    nb = (L + 7) // 8
+    unc = rng.integers(0, 256, (frames, nb), dtype=np.uint8)
+    if L % 8:
+        unc[:, -1] &= np.uint8((0xFF << (8 - L % 8)) & 0xFF)
+    bits = np.unpackbits(unc, axis=1)[:, :L]
+    coded = encode_bits(K, g if g is not None else CODES[K], bits, orc)
+    T = L + K - 1
+    if not soft:
+        flips = (rng.random((frames, T, 2)) < p).astype(np.uint8)
+        return unc, (coded ^ (flips[..., 0] | (flips[..., 1] << 1))).astype(np.uint8)
+    b = np.stack([coded & 1, (coded >> 1) & 1], axis=-1).astype(np.float64)
+    y = (1.0 - 2.0 * b) + (sigma if sigma is not None else 0.5) * rng.standard_normal(b.shape)
+    q = np.clip(np.rint((1.0 - y) * 0.5 * 255.0), 0, 255).astype(np.uint8)
+    return unc, q
+
+
+def encode_bits(K, g, bits, orc=None):
+    """Terminated encoding of arbitrary-length bit rows (vectorised restatement of
+    convEncode.c:46-130; whole-byte rows are cross-checked against the oracle encoder)."""
+    bits = np.asarray(bits, np.uint8)
+    F, L = bits.shape
+    S = K - 1
+    padded = np.concatenate([np.zeros((F, S), np.uint8), bits, np.zeros((F, S), np.uint8)], axis=1)
+    T = L + S
+    # tapped-delay bit i (i steps ago) at step t is padded[:, t + S - i]
+    revs = []
+    for gi in g:
+        rv = [(gi >> (K - 1 - i)) & 1 for i in range(K)]  # reversed: bit i of poly = MSB-i of g
+        revs.append(rv)
+    out = np.zeros((F, T), np.uint8)
+    for j, rv in enumerate(revs):
+        acc = np.zeros((F, T), np.uint8)
+        for i in range(K):
+            if rv[i]:
+                acc ^= padded[:, S - i:S - i + T]
+        out |= (acc << j).astype(np.uint8)
+    return out
+
+
+def hard_to_soft(rx):
+    """Map hard segments to the soft format's hard-equivalent input q = 255*bit."""
+    rx = np.asarray(rx, np.uint8)
+    return np.stack([(rx & 1) * 255, ((rx >> 1) & 1) * 255], axis=-1).astype(np.uint8)

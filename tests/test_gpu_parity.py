@@ -1,0 +1,230 @@
+"""GPU parity: the HIP decoder (called through the C ABI) against the reference's golden
+vectors, the reference's berTestK7 known-answer counts and the oracle on seeded inputs.
+Bit-exact everywhere (integer work)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from helpers import (BERTEST_ERRORS, CODES, Oracle, golden_sets, hard_to_soft, load_golden, manifest, random_frames)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, native  # noqa: E402
+
+KERNELS = ("auto", "lds")
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+@pytest.fixture(params=KERNELS)
+def kernel(request, monkeypatch):
+    if request.param == "auto":
+        monkeypatch.delenv("VTB_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("VTB_KERNEL", request.param)
+    return request.param
+
+
+def dev_decode(dec, frames):
+    x = torch.from_numpy(np.ascontiguousarray(frames).reshape(frames.shape[0], -1)).cuda()
+    out = dec.decode_device(x)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("K", [5, 7, 9])
+def test_hard_golden_vectors(K, kernel):
+    for key, L, unc, rx, dec in golden_sets(K):
+        d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
+        assert (d.decode_host(rx) == dec).all(), (K, key)
+        assert (dev_decode(d, rx) == dec).all(), (K, key)
+
+
+@pytest.mark.parametrize("K", [5, 7, 9])
+def test_soft_bridge_golden_vectors(K, kernel):
+    """Soft input q = 255*bit must reproduce the reference's hard decode bit for bit."""
+    for key, L, unc, rx, dec in golden_sets(K):
+        d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True)
+        assert (dev_decode(d, hard_to_soft(rx)) == dec).all(), (K, key)
+
+
+@pytest.mark.parametrize("K,g", [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]), (9, CODES[9])])
+@pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048])
+def test_hard_random_vs_oracle(orc, K, g, L, kernel):
+    for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
+        unc, rx = random_frames(orc, K, L, 257, p, seed + L, g=g)
+        expect = orc.decode(K, g, rx, L)
+        got = ViterbiDecoder(ConvCode(K, g), frame_bits=L).decode_host(rx)
+        assert (got == expect).all(), (K, L, p)
+        if p == 0.0:
+            assert (got == unc).all()
+
+
+@pytest.mark.parametrize("K", [5, 7, 9])
+@pytest.mark.parametrize("L", [9, 1024, 2048])
+def test_soft_random_vs_oracle(orc, K, L, kernel):
+    for sigma, seed in ((0.4994, 21), (0.6287, 22), (1.5, 23)):
+        unc, q = random_frames(orc, K, L, 193, 0.0, seed + L, soft=True, sigma=sigma)
+        expect = orc.decode(K, CODES[K], q, L, soft=True)
+        got = dev_decode(ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True), q)
+        assert (got == expect).all(), (K, L, sigma)
+
+
+def test_soft_extreme_values(orc, kernel):
+    """Saturated, constant and alternating soft inputs (tie-heavy) match the oracle."""
+    K, L = 7, 512
+    T = L + K - 1
+    rng = np.random.default_rng(7)
+    cases = [np.zeros((4, T, 2), np.uint8), np.full((4, T, 2), 255, np.uint8), np.full((4, T, 2), 128, np.uint8),
+             np.full((4, T, 2), 127, np.uint8), rng.choice(np.array([0, 127, 128, 255], np.uint8), (64, T, 2))]
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True)
+    for q in cases:
+        assert (dev_decode(d, q) == orc.decode(K, CODES[K], q, L, soft=True)).all()
+
+
+def test_bertest_k7_kat_on_gpu(orc, kernel):
+    """The reference berTestK7 stream (glibc rand seed 9865, 3 x 10000 packets) decoded on
+    the GPU gives exactly the reference's decoded bit-error counts."""
+    unc, rx, _ = orc.bertest()
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=2048)
+    for c in range(3):
+        out = dev_decode(d, rx[c])
+        assert int(np.unpackbits(unc[c] ^ out).sum()) == BERTEST_ERRORS[c]
+
+
+def test_full_size_soft_batch_properties(orc):
+    """BASELINE config C3 at full size: 65536 x 2048-bit soft frames.  Noise-free frames
+    decode to the payload exactly; a noisy batch decodes identically on two launches and a
+    strided subset matches the oracle."""
+    from helpers import encode_bits
+
+    K, L, F, U = 7, 2048, 65536, 4096
+    rng = np.random.default_rng(2024)
+    unc = rng.integers(0, 256, (U, L // 8), dtype=np.uint8)
+    q = hard_to_soft(encode_bits(K, CODES[K], np.unpackbits(unc, axis=1)))
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True)
+    x = torch.from_numpy(q.reshape(U, -1)).cuda().repeat(F // U, 1)
+    out = d.decode_device(x).cpu().numpy()
+    assert (out == np.tile(unc, (F // U, 1))).all()
+    noisy = np.clip(q.astype(np.int16) + rng.integers(-150, 150, q.shape, dtype=np.int16), 0, 255).astype(np.uint8)
+    xn = torch.from_numpy(noisy.reshape(U, -1)).cuda().repeat(F // U, 1)
+    o1 = d.decode_device(xn)
+    o2 = d.decode_device(xn)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    o1 = o1.cpu().numpy()
+    assert (o1[:U] == o1[F - U:]).all()
+    sub = np.arange(0, U, 61)
+    assert (o1[sub] == orc.decode(K, CODES[K], noisy[sub], L, soft=True)).all()
+
+
+def test_k9_full_config(orc, kernel):
+    """C4: K=9 hard, 4096 x 1024 -- oracle on a strided subset, round trip on all."""
+    K, L, F = 9, 1024, 4096
+    unc, rx = random_frames(orc, K, L, F, 0.03, 99)
+    got = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L).decode_host(rx)
+    sub = np.arange(0, F, 37)
+    assert (got[sub] == orc.decode(K, CODES[K], rx[sub], L)).all()
+    ber = np.unpackbits(got ^ unc).mean()
+    assert ber < 1e-3
+
+
+def test_strided_device_io(orc):
+    K, L, F = 7, 640, 300
+    unc, rx = random_frames(orc, K, L, F, 0.05, 5)
+    T = L + K - 1
+    big = np.zeros((F, T + 37), np.uint8)
+    big[:, :T] = rx
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
+    x = torch.from_numpy(big).cuda()[:, :T]
+    out = torch.zeros((F, 128), dtype=torch.uint8, device="cuda")
+    lib = native.lib()
+    rc = lib.vtb_decode_device(d._plan, ctypes.c_void_p(x.data_ptr()), x.stride(0), ctypes.c_void_p(out.data_ptr()),
+                               out.stride(0), F, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy()[:, :L // 8] == orc.decode(K, CODES[K], rx, L)).all()
+    assert (out.cpu().numpy()[:, L // 8:] == 0).all()
+    # strides smaller than a frame are rejected, zero frames is a no-op
+    assert lib.vtb_decode_device(d._plan, ctypes.c_void_p(x.data_ptr()), T - 1, ctypes.c_void_p(out.data_ptr()), 128,
+                                 F, None) == native.VTB_ERR_INVALID
+    assert lib.vtb_decode_device(d._plan, None, 0, None, 0, 0, None) == 0
+
+
+def test_multi_device_host_api(orc):
+    K, L, F = 7, 256, 1000
+    unc, rx = random_frames(orc, K, L, F, 0.04, 8)
+    assert (decode_multi(rx, ConvCode(K, CODES[K]), L) == orc.decode(K, CODES[K], rx, L)).all()
+
+
+# ---------------- legacy C API (include/viterbiDecoder.h) on the GPU ----------------
+
+def _legacy(K):
+    from convolutionalencdec_amd import LIB_DIR
+
+    L = ctypes.CDLL(os.path.join(LIB_DIR, f"libviterbi_legacy_k{K}.so"))
+    v = ctypes.c_void_p
+    L.viterbiInitButterflyk1.argtypes = [v]
+    L.resetViterbiDecoderHardButterflyk1.argtypes = [v]
+    L.viterbiDecoderHardButterflyk1.argtypes = [v, v, v, ctypes.c_int, ctypes.c_bool]
+    L.viterbiConfigCheck.argtypes = []
+    return L
+
+
+def _state(K):
+    size = manifest()["kat"]["viterbiHardState_t_sizeof"][str(K)]
+    buf = np.zeros(size + 64, np.uint8)
+    off = (-buf.ctypes.data) % 64
+    return buf, ctypes.c_void_p(buf.ctypes.data + off)
+
+
+@pytest.mark.parametrize("K", [5, 7, 9])
+def test_legacy_api_golden(K):
+    lib = _legacy(K)
+    buf, st = _state(K)
+    lib.resetViterbiDecoderHardButterflyk1(st)
+    lib.viterbiInitButterflyk1(st)
+    assert lib.viterbiConfigCheck() == 0
+    for key, L, unc, rx, dec in golden_sets(K):
+        for f in range(0, rx.shape[0], 5):
+            out = np.zeros(dec.shape[1], np.uint8)
+            row = np.ascontiguousarray(rx[f])
+            r = lib.viterbiDecoderHardButterflyk1(st, row.ctypes.data_as(ctypes.c_void_p),
+                                                  out.ctypes.data_as(ctypes.c_void_p), len(row), True)
+            assert r == (L - 1) // 8 + 1
+            assert (out == dec[f]).all(), (key, f)
+
+
+def test_legacy_api_streaming_chunks():
+    """last=false chunks are accumulated; the last=true call decodes the whole frame."""
+    lib = _legacy(7)
+    buf, st = _state(7)
+    lib.resetViterbiDecoderHardButterflyk1(st)
+    lib.viterbiInitButterflyk1(st)
+    z = load_golden("stream_metrics.npz")
+    rx, dec = z["k7_f0_rx"], z["k7_f0_decoded"]
+    out = np.zeros(dec.shape, np.uint8)
+    c = 0
+    while len(rx) - c > 7:
+        chunk = np.ascontiguousarray(rx[c:c + 7])
+        assert lib.viterbiDecoderHardButterflyk1(st, chunk.ctypes.data_as(ctypes.c_void_p),
+                                                 out.ctypes.data_as(ctypes.c_void_p), 7, False) == 0
+        c += 7
+    rest = np.ascontiguousarray(rx[c:])
+    r = lib.viterbiDecoderHardButterflyk1(st, rest.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
+                                          len(rest), True)
+    assert r == dec.shape[0]
+    assert (out == dec).all()
