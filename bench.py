@@ -93,7 +93,15 @@ def cpu_baseline(seconds, threads, frame_bits):
         lib = ctypes.CDLL(ref)
         lib.ref_speed.restype = ctypes.c_double
         lib.ref_speed.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int]
-        mbps = lib.ref_speed(seconds, threads, pkt_bytes)
+        # The reference's VITERBI_INIT prints to stdout; keep stdout for the one JSON line.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            mbps = lib.ref_speed(seconds, threads, pkt_bytes)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
                 "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
                           f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "

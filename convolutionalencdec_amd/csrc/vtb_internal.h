@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace vtb {
 
@@ -24,6 +25,13 @@ struct Launch {
     hipStream_t stream = nullptr;
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
+
+// Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS).  Never
+// set in production; outputs are garbage when set.
+inline int debug_flags() {
+    const char* v = getenv("VTB_DEBUG");
+    return v ? atoi(v) : 0;
+}
 
 // Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
 // shape limits are reported through *_supported() beforehand.

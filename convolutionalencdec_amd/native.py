@@ -8,7 +8,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libviterbi_amd.so")
+# $VTB_LIB_PATH points at an alternative build (A/B measurement of kernel variants only).
+LIB_PATH = os.environ.get("VTB_LIB_PATH") or os.path.join(LIB_DIR, "libviterbi_amd.so")
 
 VTB_OK = 0
 VTB_ERR_INVALID = -1

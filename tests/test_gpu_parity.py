@@ -62,8 +62,10 @@ def test_soft_bridge_golden_vectors(K, kernel):
 
 
 @pytest.mark.parametrize("K,g", [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]), (9, CODES[9])])
-@pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048])
+@pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000])
 def test_hard_random_vs_oracle(orc, K, g, L, kernel):
+    if L > 4096 and K not in (5, 7):
+        pytest.skip("survivor memory of this K and L exceeds one CU's LDS (DESIGN.md, frame-length limits)")
     for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
         unc, rx = random_frames(orc, K, L, 257, p, seed + L, g=g)
         expect = orc.decode(K, g, rx, L)

@@ -1,11 +1,31 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, bench (+ optional rocprofv3 kernel-trace summary).
+# Usage (through gpurun): bash tools/gpu_check.sh [tests] [smoke] [bench] [prof] [pmc]
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-rocminfo 2>/dev/null | grep -m3 -E 'gfx|Marketing' > gpurun_out/devinfo.txt || true
-nproc > gpurun_out/nproc.txt
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 5 > gpurun_out/bench.log 2>&1 || exit $?
+steps="${*:-tests smoke bench}"
+export TMPDIR=/tmp
+for s in $steps; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/gpu_tests.log 2>&1
+      rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
+      [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $? ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 50 --warmup 5 --cpu-seconds 5 > gpurun_out/bench.log 2>&1 || exit $?
+      VTB_KERNEL=lds timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/bench_lds.log 2>&1 || exit $?
+      timeout -k 10 300 python bench.py --steps 50 --warmup 5 --cpu-seconds 0 --hard > gpurun_out/bench_hard.log 2>&1 || exit $?
+      timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 0 --frames 65536 > gpurun_out/bench_65k.log 2>&1 || exit $? ;;
+    prof)
+      rm -rf gpurun_out/prof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 > gpurun_out/prof.log 2>&1 || exit $? ;;
+    pmc)
+      rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $? ;;
+  esac
+done
+exit 0
