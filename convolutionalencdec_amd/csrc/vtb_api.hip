@@ -31,6 +31,9 @@ struct vtb_plan {
     uint8_t* d_out = nullptr;
     size_t cap_frames = 0;
     hipStream_t stream = nullptr;
+    // kernel workspace (survivor words), stream-ordered pool memory, grown on demand
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
 };
 
 namespace {
@@ -82,7 +85,7 @@ bool env_flag_is(const char* name, const char* value) {
 
 // Which kernel family a plan uses: the register path when it supports the shape, else
 // the LDS path.  VTB_KERNEL=lds|reg forces one (testing / A-B measurement).
-int launch(const vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
+int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
            size_t frames, hipStream_t stream) {
     vtb::Launch a;
     a.S = p->code.constraint_length - 1;
@@ -100,12 +103,25 @@ int launch(const vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_
     const bool force_reg = env_flag_is("VTB_KERNEL", "reg");
     hipError_t e;
     if (!force_lds && vtb::reg_path_supported(a)) {
+        const size_t need = vtb::reg_path_workspace_bytes(a);
+        if (need > p->ws_bytes) {
+            if (p->ws) (void)vtb::workspace_free(p->ws, stream);
+            p->ws = nullptr;
+            p->ws_bytes = 0;
+            if (vtb::workspace_alloc(&p->ws, need, stream) != hipSuccess) {
+                p->ws = nullptr;
+                return VTB_ERR_NOMEM;
+            }
+            p->ws_bytes = need;
+        }
+        a.ws = p->ws;
         e = vtb::launch_reg_path(a);
     } else if (!force_reg && vtb::lds_path_supported(a)) {
         e = vtb::launch_lds_path(a);
     } else {
         return VTB_ERR_UNSUPPORTED;
     }
+    if (e == hipErrorOutOfMemory) return VTB_ERR_NOMEM;
     return e == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
 }
 
@@ -128,6 +144,44 @@ bool device_is_gfx950(int dev) {
 }
 
 }  // namespace
+
+namespace vtb {
+
+namespace {
+std::mutex g_pool_mutex;
+hipMemPool_t g_pools[64] = {};
+}  // namespace
+
+hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    hipMemPool_t pool;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mutex);
+        if (!g_pools[dev]) {
+            hipMemPoolProps props = {};
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            e = hipMemPoolCreate(&g_pools[dev], &props);
+            if (e != hipSuccess) {
+                g_pools[dev] = nullptr;
+                return e;
+            }
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(g_pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        pool = g_pools[dev];
+    }
+    return hipMallocFromPoolAsync(p, bytes, pool, stream);
+}
+
+hipError_t workspace_free(void* p, hipStream_t stream) { return hipFreeAsync(p, stream); }
+
+}  // namespace vtb
 
 extern "C" {
 
@@ -209,6 +263,11 @@ void vtb_plan_destroy(vtb_plan_t* plan) {
     DeviceGuard g(plan->device);
     if (plan->d_in) (void)hipFree(plan->d_in);
     if (plan->d_out) (void)hipFree(plan->d_out);
+    if (plan->ws) {
+        (void)hipDeviceSynchronize();  // launches on any stream may still use it
+        (void)vtb::workspace_free(plan->ws, nullptr);
+        (void)hipStreamSynchronize(nullptr);
+    }
     if (plan->stream) (void)hipStreamDestroy(plan->stream);
     delete plan;
 }

@@ -23,6 +23,7 @@ struct Launch {
     size_t out_stride = 0;
     size_t frames = 0;
     hipStream_t stream = nullptr;
+    void* ws = nullptr;  // device workspace of at least *_workspace_bytes() (plan-owned)
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
@@ -39,6 +40,12 @@ bool lds_path_supported(const Launch& a);
 hipError_t launch_lds_path(const Launch& a);
 
 bool reg_path_supported(const Launch& a);
+size_t reg_path_workspace_bytes(const Launch& a);
 hipError_t launch_reg_path(const Launch& a);
+
+// Stream-ordered scratch memory from a per-device pool that keeps its memory (no release
+// back to the driver between launches), so a per-launch workspace costs no hipMalloc.
+hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream);
+hipError_t workspace_free(void* p, hipStream_t stream);
 
 }  // namespace vtb

@@ -91,7 +91,9 @@ void vtb_plan_destroy(vtb_plan_t* plan);
 
 /* Decode `frames` frames already resident in device memory, asynchronously on `stream`
  * (a hipStream_t; NULL = default stream).  d_in: frames * in_stride bytes; d_out: frames *
- * out_stride bytes.  Strides >= the per-frame sizes above. */
+ * out_stride bytes.  Strides >= the per-frame sizes above.  The plan's survivor workspace
+ * (8 bytes per frame per trellis step, grown on demand, stream-ordered) is shared by its
+ * launches: calls on one plan must use one stream, or the caller orders them. */
 int vtb_decode_device(vtb_plan_t* plan, const uint8_t* d_in, size_t in_stride, uint8_t* d_out,
                       size_t out_stride, size_t frames, void* stream);
 

@@ -12,11 +12,9 @@ build() {
 for v in "$@"; do
   case $v in
     nostore) build nostore -DVTB_EXP_NO_STORE ;;
-    nodecide) build nodecide -DVTB_EXP_NO_DECIDE ;;
-    noexch) build noexch -DVTB_EXP_NO_EXCHANGE ;;
-    bare) build bare -DVTB_EXP_NO_DECIDE -DVTB_EXP_NO_EXCHANGE ;;
-    warm96) build warm96 -DVTB_WARM=96 ;;
-    warm144) build warm144 -DVTB_WARM=144 ;;
+    nolds) build nolds -DVTB_EXP_NO_LDS ;;
+    nocmp) build nocmp -DVTB_EXP_NO_CMP ;;
+    nostore_nolds) build nostore_nolds -DVTB_EXP_NO_STORE -DVTB_EXP_NO_LDS ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

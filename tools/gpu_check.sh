@@ -21,11 +21,11 @@ for s in $steps; do
       timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 0 --frames 65536 > gpurun_out/bench_65k.log 2>&1 || exit $? ;;
     prof)
       rm -rf gpurun_out/prof
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 > gpurun_out/prof.log 2>&1 || exit $? ;;
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 > gpurun_out/prof.log 2>&1 || exit $? ;;
     pmc)
       rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
-      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
-      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $? ;;
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $? ;;
   esac
 done
 exit 0
