@@ -1,8 +1,8 @@
 // C-ABI implementation of include/viterbi_amd.h: code tables, plans, kernel choice,
 // host/device entry points and the multi-GPU shard driver.
 //
-// Host-side only; the trellis work happens in the kernels of vtb_reg_path.hip (fast
-// register-resident path) and vtb_lds_path.hip (baseline path, every K).
+// Host-side only; the trellis work happens in the kernels of vtb_k7_lds.hip (K=7, the fast
+// path), vtb_reg_path.hip (K=7, long frames) and vtb_lds_path.hip (every K).
 
 #include <hip/hip_runtime.h>
 
@@ -83,8 +83,8 @@ bool env_flag_is(const char* name, const char* value) {
     return v && std::strcmp(v, value) == 0;
 }
 
-// Which kernel family a plan uses: the register path when it supports the shape, else
-// the LDS path.  VTB_KERNEL=lds|reg forces one (testing / A-B measurement).
+// Which kernel family a plan uses (see below).  VTB_KERNEL=k7|gws|lds forces one (testing
+// and A/B measurement); a forced kernel that does not support the shape is an error.
 int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
            size_t frames, hipStream_t stream) {
     vtb::Launch a;
@@ -99,10 +99,17 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.frames = frames;
     a.stream = stream;
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
-    const bool force_lds = env_flag_is("VTB_KERNEL", "lds");
-    const bool force_reg = env_flag_is("VTB_KERNEL", "reg");
+    const char* force = std::getenv("VTB_KERNEL");
+    const bool any = !force || !*force;
+    const bool want_k7 = any || env_flag_is("VTB_KERNEL", "k7");
+    const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
+    const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
     hipError_t e;
-    if (!force_lds && vtb::reg_path_supported(a)) {
+    // LDS-resident K=7 kernel while it keeps at least 4 waves per CU (2 frames per wave),
+    // else the global-workspace K=7 kernel, else the generic LDS-path kernel (every K).
+    if (want_k7 && vtb::k7_lds_supported(a) && (!any || vtb::k7_lds_bytes(a) <= 40 * 1024)) {
+        e = vtb::launch_k7_lds(a);
+    } else if (want_gws && vtb::reg_path_supported(a)) {
         const size_t need = vtb::reg_path_workspace_bytes(a);
         if (need > p->ws_bytes) {
             if (p->ws) (void)vtb::workspace_free(p->ws, stream);
@@ -116,7 +123,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
         }
         a.ws = p->ws;
         e = vtb::launch_reg_path(a);
-    } else if (!force_reg && vtb::lds_path_supported(a)) {
+    } else if (want_lds && vtb::lds_path_supported(a)) {
         e = vtb::launch_lds_path(a);
     } else {
         return VTB_ERR_UNSUPPORTED;
@@ -250,7 +257,7 @@ int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input
     a.soft = input == VTB_INPUT_SOFT8;
     a.T = p->T;
     a.L = p->L;
-    if (!vtb::reg_path_supported(a) && !vtb::lds_path_supported(a)) {
+    if (!vtb::k7_lds_supported(a) && !vtb::reg_path_supported(a) && !vtb::lds_path_supported(a)) {
         delete p;
         return VTB_ERR_UNSUPPORTED;
     }

@@ -39,6 +39,12 @@ inline int debug_flags() {
 bool lds_path_supported(const Launch& a);
 hipError_t launch_lds_path(const Launch& a);
 
+// K=7, survivors in LDS (vtb_k7_lds.hip): the fast path.
+bool k7_lds_supported(const Launch& a);
+size_t k7_lds_bytes(const Launch& a);
+hipError_t launch_k7_lds(const Launch& a);
+
+// K=7, survivors in a global workspace (vtb_reg_path.hip): long frames.
 bool reg_path_supported(const Launch& a);
 size_t reg_path_workspace_bytes(const Launch& a);
 hipError_t launch_reg_path(const Launch& a);

@@ -15,7 +15,15 @@ torch = pytest.importorskip("torch")
 
 from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, native  # noqa: E402
 
-KERNELS = ("auto", "lds")
+# "auto": the library's own choice; the others force one kernel family: "k7" (K=7,
+# survivors in LDS), "gws" (K=7, survivors in a global workspace), "lds" (every K).
+KERNELS = ("auto", "k7", "gws", "lds")
+
+
+class Kern(str):
+    def need(self, K):
+        if self in ("k7", "gws") and K != 7:
+            pytest.skip(f"kernel {self} is K=7 only")
 
 
 @pytest.fixture(scope="module")
@@ -35,7 +43,7 @@ def kernel(request, monkeypatch):
         monkeypatch.delenv("VTB_KERNEL", raising=False)
     else:
         monkeypatch.setenv("VTB_KERNEL", request.param)
-    return request.param
+    return Kern(request.param)
 
 
 def dev_decode(dec, frames):
@@ -47,6 +55,7 @@ def dev_decode(dec, frames):
 
 @pytest.mark.parametrize("K", [5, 7, 9])
 def test_hard_golden_vectors(K, kernel):
+    kernel.need(K)
     for key, L, unc, rx, dec in golden_sets(K):
         d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
         assert (d.decode_host(rx) == dec).all(), (K, key)
@@ -56,6 +65,7 @@ def test_hard_golden_vectors(K, kernel):
 @pytest.mark.parametrize("K", [5, 7, 9])
 def test_soft_bridge_golden_vectors(K, kernel):
     """Soft input q = 255*bit must reproduce the reference's hard decode bit for bit."""
+    kernel.need(K)
     for key, L, unc, rx, dec in golden_sets(K):
         d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True)
         assert (dev_decode(d, hard_to_soft(rx)) == dec).all(), (K, key)
@@ -64,6 +74,7 @@ def test_soft_bridge_golden_vectors(K, kernel):
 @pytest.mark.parametrize("K,g", [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]), (9, CODES[9])])
 @pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000])
 def test_hard_random_vs_oracle(orc, K, g, L, kernel):
+    kernel.need(K)
     if L > 4096 and K not in (5, 7):
         pytest.skip("survivor memory of this K and L exceeds one CU's LDS (DESIGN.md, frame-length limits)")
     for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
@@ -78,6 +89,7 @@ def test_hard_random_vs_oracle(orc, K, g, L, kernel):
 @pytest.mark.parametrize("K", [5, 7, 9])
 @pytest.mark.parametrize("L", [9, 1024, 2048])
 def test_soft_random_vs_oracle(orc, K, L, kernel):
+    kernel.need(K)
     for sigma, seed in ((0.4994, 21), (0.6287, 22), (1.5, 23)):
         unc, q = random_frames(orc, K, L, 193, 0.0, seed + L, soft=True, sigma=sigma)
         expect = orc.decode(K, CODES[K], q, L, soft=True)
@@ -136,6 +148,7 @@ def test_full_size_soft_batch_properties(orc):
 def test_k9_full_config(orc, kernel):
     """C4: K=9 hard, 4096 x 1024 -- oracle on a strided subset, round trip on all."""
     K, L, F = 9, 1024, 4096
+    kernel.need(K)
     unc, rx = random_frames(orc, K, L, F, 0.03, 99)
     got = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L).decode_host(rx)
     sub = np.arange(0, F, 37)

@@ -7,7 +7,7 @@ build() {
   name=$1; shift
   d=convolutionalencdec_amd/lib/exp/$name; mkdir -p $d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -I$CS "$@" \
-      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_reg_path.hip
+      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_reg_path.hip $CS/vtb_k7_lds.hip
 }
 for v in "$@"; do
   case $v in
@@ -15,6 +15,9 @@ for v in "$@"; do
     nolds) build nolds -DVTB_EXP_NO_LDS ;;
     nocmp) build nocmp -DVTB_EXP_NO_CMP ;;
     nostore_nolds) build nostore_nolds -DVTB_EXP_NO_STORE -DVTB_EXP_NO_LDS ;;
+    nostage) build nostage -DVTB_EXP_NO_STAGE ;;
+    noword) build noword -DVTB_EXP_NO_WORD ;;
+    nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

@@ -13,6 +13,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_INSTS SQ_ACTIVE_INST_VALU2 SQ_INST_LEVEL_SMEM SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   rm -rf gpurun_out/pmc_sq$i
-  VTB_DEBUG=$dbg timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc_sq$i -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_sq$i.log 2>&1 || exit $?
+  VTB_DEBUG=$dbg timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc_sq$i -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 ${PMC_BENCH_ARGS:-} > gpurun_out/pmc_sq$i.log 2>&1 || exit $?
 done
 exit 0
