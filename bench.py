@@ -13,8 +13,10 @@ the rank's batch.  Frames are independent, so ranks share nothing on the data pa
 max-over-ranks reduction of the elapsed time.
 
 Prints ONE JSON line on rank 0 (the driver's contract), with the roofline of the decode
-kernel (HIP-event time per launch, algorithmic bytes per launch) and the CPU baseline
-(the reference's own decoder, oracle/_ref, timed on this host's cores at N=1).
+kernel (HIP-event time per launch on the launch stream, algorithmic bytes per launch, HBM
+bytes per launch from profiles/pmc_traffic.json) and the CPU baseline (the reference's own
+decoder, oracle/_ref, timed on this host's cores at N=1).  dtype "u16": the decoder's path
+metrics are packed unsigned 16-bit integers.
 """
 import argparse
 import ctypes
@@ -223,7 +225,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "u16",
         "data": "synthetic",
         "config": {
             "workload": f"K={code[0]} r=1/2 {'8-bit soft' if soft else 'hard'}-decision Viterbi, {F} frames x {L} "
@@ -244,6 +246,9 @@ def main():
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 5),
             "algorithmic_bytes_per_launch": alg_bytes,
+            # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)
+            "secondary": {"bound": "valu", "state_steps_per_s": round(F * (1 << (code[0] - 1)) * T / (kern_ms * 1e-3)),
+                          "note": "packed u16 ACS, 2 frames per wave64; see DESIGN.md 5"},
         },
         "cpu_baseline": cpu,
     }

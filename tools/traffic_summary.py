@@ -1,0 +1,47 @@
+"""HBM traffic per launch from the two rocprofv3 --pmc passes of tools/gpu_check.sh pmc
+(FETCH_SIZE and WRITE_SIZE, KiB per dispatch, summed over the XCDs by rocprofv3).
+
+Writes profiles/pmc_traffic.json: {workload_key: bytes_per_launch}, read by bench.py for
+roofline.traffic, plus profiles/<round>/pmc_traffic_detail.json with the raw numbers.
+FETCH_SIZE/WRITE_SIZE count the L2's memory-side requests (Infinity-Cache hits included);
+MI355X_MICROARCH.md: gfx950 FETCH_SIZE counts 128-B read requests as 64 B, i.e. half the
+bytes of a coalesced streaming read.  This kernel's input loads are coalesced 2-byte loads
+and the raw FETCH_SIZE came out at 0.517x the input bytes (4,467,188 of 8,437,760 at
+K7_soft_F4096_L1024), the same halving, so the fetch figure is doubled; WRITE_SIZE matched
+the output bytes exactly (524,288) and is used as is.
+"""
+import csv
+import json
+import os
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+key = sys.argv[3] if len(sys.argv) > 3 else "K7_soft_F4096_L1024"
+repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def mean_counter(d, name):
+    vals = []
+    for r in csv.DictReader(open(os.path.join(root, d, "run_counter_collection.csv"))):
+        if r["Counter_Name"] == name and "kernel" in r["Kernel_Name"]:
+            vals.append(float(r["Counter_Value"]))
+    return sum(vals) / len(vals), len(vals)
+
+
+fetch_kib, nf = mean_counter("pmc_fetch", "FETCH_SIZE")
+write_kib, nw = mean_counter("pmc_write", "WRITE_SIZE")
+FETCH_CORRECTION = 2.0
+total = (FETCH_CORRECTION * fetch_kib + write_kib) * 1024.0
+os.makedirs(os.path.join(repo, "profiles", rnd), exist_ok=True)
+with open(os.path.join(repo, "profiles", rnd, "pmc_traffic_detail.json"), "w") as fh:
+    json.dump({"workload": key, "fetch_kib_per_dispatch_raw": fetch_kib, "fetch_correction": FETCH_CORRECTION,
+               "write_kib_per_dispatch": write_kib,
+               "dispatches": [nf, nw], "bytes_per_launch": total}, fh, indent=1)
+path = os.path.join(repo, "profiles", "pmc_traffic.json")
+data = {}
+if os.path.exists(path):
+    data = json.load(open(path))
+data[key] = round(total)
+json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+print(key, "fetch KiB", fetch_kib, "write KiB", write_kib, "bytes/launch", total)
