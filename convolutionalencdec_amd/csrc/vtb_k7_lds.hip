@@ -63,6 +63,7 @@ namespace {
 using namespace k7;
 
 constexpr int kHalf = 24;     // table rows staged at a time (ring of 2 halves = kChunk rows)
+constexpr int kRowBytes = 32; // branch-metric table row: (V, W) of the four edge labels
 constexpr int kTbWarm = 48;   // traceback warm-up steps past a block's end
 
 int tb_block(int T) {
@@ -72,7 +73,7 @@ int tb_block(int T) {
 int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
-int region0(int T) { return 8 * tb_block(T) > kChunk * kTabBytes ? 8 * tb_block(T) : kChunk * kTabBytes; }
+int region0(int T) { return 8 * tb_block(T) > kChunk * kRowBytes ? 8 * tb_block(T) : kChunk * kRowBytes; }
 size_t lds_bytes(int T) { return (size_t)region0(T) + 16 * (size_t)t_pad(T); }
 
 // lane <-> location map (an involution)
@@ -88,6 +89,35 @@ __device__ __forceinline__ uint32_t exch_plus(uint32_t m, uint32_t w) {
     }
 }
 
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (a & mask) | (b & ~mask); }
+
+// The candidates of a step: A = own metric + V, B = partner's metric + W, and A1 = A + R
+// (R = 1 in both halves for lanes whose own state is the upper predecessor), so that
+// [A1 > B] is the reference's decision rule for either lane of a butterfly.  For the
+// permlane phases the add of A separates the last write of M from the swap and the add of
+// A1 separates the swap from the read of its result, inside one asm block (the swap needs
+// one wait state after a VALU write of its operand: permlane_hazard probe).
+template <int P>
+__device__ __forceinline__ void acs_pair(uint32_t m, uint2 vw, uint32_t r, uint32_t& A, uint32_t& A1, uint32_t& B) {
+    if constexpr (P == 4 || P == 5) {
+        if constexpr (P == 4) {
+            asm volatile("v_add_u32 %0, %2, %3\n\tv_permlane16_swap_b32 %2, %2\n\tv_add_u32 %1, %0, %4"
+                         : "=&v"(A), "=&v"(A1), "+v"(m) : "v"(vw.x), "v"(r));
+        } else {
+            asm volatile("v_add_u32 %0, %2, %3\n\tv_permlane32_swap_b32 %2, %2\n\tv_add_u32 %1, %0, %4"
+                         : "=&v"(A), "=&v"(A1), "+v"(m) : "v"(vw.x), "v"(r));
+        }
+        B = m + vw.y;
+    } else {
+        A = m + vw.x;
+        A1 = A + r;
+        B = exch_plus<P>(m, vw.y);
+    }
+}
+
+// Bit of step s (0..15) of a frame in its 16-bit half of a decision word (see the ACS).
+constexpr int word_bit(int s) { return 8 * (s & 1) + 7 - (s >> 1); }
+
 // 48 traceback steps over steps [tlo, tlo + 48) (tlo a multiple of 48), newest first, on
 // the lane index lam of the survivor's location.  Returns the 48 decoded bits (MSB = step
 // tlo): each sextet's bits are its starting location.
@@ -96,7 +126,7 @@ __device__ __forceinline__ uint64_t tb_body(const uint8_t* decf, int tlo, uint32
     uint64_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 48; j++) {
-        const int s = (47 - j) & 15;  // bit of step t = tlo + 47 - j in its word
+        const int s = word_bit((47 - j) & 15);  // bit of step t = tlo + 47 - j in its half-word
         const int p = j % 6;          // pairing bit of that step
         if (p == 0) bits |= uint64_t(lane_of(lam)) << (6 * (j / 6));
         const uint32_t w = *reinterpret_cast<const unsigned short*>(base + ((47 - j) >> 4) * 256 + lam * 4);
@@ -128,7 +158,7 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 #define VTB_EXP_STAGE true
 #endif
 #ifdef VTB_EXP_NO_WORD
-#define VTB_EXP_WORD(x) asm volatile("" ::"v"(acc))
+#define VTB_EXP_WORD(x) asm volatile("" ::"v"(z), "v"(z_p))
 #else
 #define VTB_EXP_WORD(x) x
 #endif
@@ -149,8 +179,18 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const uint8_t* inA = in + fa * in_stride;
     const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;
 
-    uint32_t off[6];
-    table_offsets(table, int(lane_of(lane)), off);
+    // Per phase: byte offset of the lane's (V, W) pair in a table row (its edge label c) and
+    // the tie bit R (bit p of the lane's location), packed for both frames.
+    uint32_t off[6], rr[6];
+    {
+        const int loc = int(lane_of(lane));
+#pragma unroll
+        for (int ph = 0; ph < 6; ph++) {
+            const int p = 5 - ph;
+            off[ph] = 8u * table.symm[rotl6(loc & ~(1 << p), ph)];
+            rr[ph] = uint32_t((loc >> p) & 1) * 0x10001u;
+        }
+    }
 
     // Table staging.  Lane r < 24 builds the rows of steps 24k + r.  The raw input bytes of
     // a chunk (48 steps: both halves, both frames) are loaded a whole chunk ahead into one of
@@ -180,21 +220,32 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     auto stage_half = [&](int h, uint32_t ra, uint32_t rb) {
         asm volatile("" : "+v"(ra), "+v"(rb));
         const int t = h * kHalf + lrow;
-        uint32_t qa, qb;
-        if constexpr (SOFT) {
-            qa = (ra & 0xffu) | ((ra & 0xff00u) << 8);
-            qb = (rb & 0xffu) | ((rb & 0xff00u) << 8);
-        } else {
-            qa = (ra & 1u) | (((ra >> 1) & 1u) << 16);
-            qb = (rb & 1u) | (((rb >> 1) & 1u) << 16);
+        // packed [frame A, frame B] received values of coded bits 0 and 1
+        uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
+        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
+        if constexpr (!SOFT) {
+            q1 = (q0 >> 1) & 0x00010001u;
+            q0 &= 0x00010001u;
         }
-        qa = t < T ? qa : 0u;
-        qb = (t < T && has_b) ? qb : 0u;
-        if (lane < kHalf) write_row<Q>(tab + ((h & 1) * kHalf + lrow) * kTabBytes, qa, qb);
+        const uint32_t keep = (t < T ? 0x0000FFFFu : 0u) | ((t < T && has_b) ? 0xFFFF0000u : 0u);
+        q0 &= keep;
+        q1 &= keep;
+        // doubled branch metrics of labels 0..3 (bit 0 of a label <-> coded bit 0):
+        // e0 = 2(q0+q1), e3 = 4Q - e0, e1 = 2(Q - q0 + q1), e2 = 2(Q + q0 - q1)
+        constexpr uint32_t R1 = 0x10001u;
+        const uint32_t e0 = (q0 + q1) << 1;
+        const uint32_t e3 = 4 * Q * R1 - e0;
+        const uint32_t dq = pk_sub(q1, q0);
+        const uint32_t e1 = pk_add(2 * Q * R1, pk_add(dq, dq));
+        const uint32_t e2 = pk_sub(2 * Q * R1, pk_add(dq, dq));
+        if (lane < kHalf) {
+            uint4* row = reinterpret_cast<uint4*>(tab + ((h & 1) * kHalf + lrow) * kRowBytes);
+            row[0] = make_uint4(e0, e3, e1, e2);  // (V, W) of labels c = 0, 1
+            row[1] = make_uint4(e2, e1, e3, e0);  // (V, W) of labels c = 2, 3
+        }
     };
 
     uint32_t M = (lane == 0) ? kBias * 0x10001u : (kBias + INIT2) * 0x10001u;
-    uint32_t acc = 0;
     Raw sa, sb;  // raw input of chunks c and c+1
     load_chunk(0, sa);
     stage_half(0, sa.a[0], sa.b[0]);
@@ -203,10 +254,14 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     uint2 cur[6], nx1[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-        cur[k] = *reinterpret_cast<const uint2*>(tab + k * kTabBytes + off[k]);
-        nx1[k] = *reinterpret_cast<const uint2*>(tab + (6 + k) * kTabBytes + off[k]);
+        cur[k] = *reinterpret_cast<const uint2*>(tab + k * kRowBytes + off[k]);
+        nx1[k] = *reinterpret_cast<const uint2*>(tab + (6 + k) * kRowBytes + off[k]);
     }
 
+    // Decision words: the 32 sign bits of 16 steps are gathered by a tree -- v_perm of the
+    // sign bytes of two steps, then three levels of shift + bit-field insert -- into one
+    // word per lane: byte 2f + (s & 1), bit 7 - (s >> 1) holds step s of frame f.
+    uint32_t d_even = 0, x_p = 0, y_p = 0, z_p = 0;
     const int tacs = (dbg & 2) ? 0 : Tpad;
     for (int t0 = 0; t0 < tacs; t0 += kChunk) {
         const int h0 = t0 / kHalf;  // half index of this chunk's first half
@@ -217,24 +272,36 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 
 #define VTB_STEP(I, PH)                                                                              \
     {                                                                                                \
-        const uint32_t A = M + cur[PH].x;                                                            \
-        const uint32_t B = exch_plus<5 - (PH)>(M, cur[PH].y);                                        \
-        const uint32_t nw = pk_min(A, B);                                                            \
-        const uint32_t d = pk_sub(B, A);                                                             \
-        acc = (d & 0x80008000u) | ((acc >> 1) & 0x7FFF7FFFu);                                      \
-        M = nw & 0xFFFEFFFEu;                                                                        \
-        if (((I) & 15) == 15) {                                                                      \
-            VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = acc);                                             \
-            const uint32_t ref = __builtin_amdgcn_readlane(M, 0);                                    \
-            const uint32_t dd = ((kBias - (ref & 0xffffu)) & 0xffffu) | ((kBias - (ref >> 16)) << 16); \
-            M = pk_add(M, dd);                                                                       \
+        uint32_t A, A1, B;                                                                           \
+        acs_pair<5 - (PH)>(M, cur[PH], rr[PH], A, A1, B);                                            \
+        M = pk_min(A, B);                                                                            \
+        const uint32_t d = pk_sub(B, A1); /* sign bits 15, 31: C = [A + R > B], frames A, B */       \
+        if (((I) & 1) == 0) {                                                                        \
+            d_even = d;                                                                              \
+        } else {                                                                                     \
+            const uint32_t x = __builtin_amdgcn_perm(d, d_even, 0x07030501u);                        \
+            if (((I) & 3) == 1) {                                                                    \
+                x_p = x;                                                                             \
+            } else {                                                                                 \
+                const uint32_t y = bfi(0x80808080u, x_p, x >> 1);                                    \
+                if (((I) & 7) == 3) {                                                                \
+                    y_p = y;                                                                         \
+                } else {                                                                             \
+                    const uint32_t z = bfi(0xC0C0C0C0u, y_p, y >> 2);                                \
+                    if (((I) & 15) == 7) {                                                           \
+                        z_p = z;                                                                     \
+                    } else {                                                                         \
+                        VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = bfi(0xF0F0F0F0u, z_p, z >> 4));       \
+                    }                                                                                \
+                }                                                                                    \
+            }                                                                                        \
         }                                                                                            \
     }
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
         uint2 nx2[6];                                                                             \
         _Pragma("unroll") for (int k = 0; k < 6; k++) nx2[k] =                                    \
-            ap[k][((6 * ((G) + 2) + k) % kChunk) * (kTabBytes / 8)];                              \
+            ap[k][((6 * ((G) + 2) + k) % kChunk) * (kRowBytes / 8)];                              \
         if ((G) == 1 && VTB_EXP_STAGE) {                                                          \
             stage_half(h0 + 1, sa.a[1], sa.b[1]);                                                 \
             load_chunk(h0 / 2 + 2, sa);                                                           \
@@ -250,13 +317,23 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
+        // renormalise once per chunk: 48 steps add at most 48 * 1020 to a doubled metric, so
+        // values stay below kBias + 6120 + 48960 < 65536
+        {
+            const uint32_t ref = __builtin_amdgcn_readlane(M, 0);
+            const uint32_t dd = ((kBias - (ref & 0xffffu)) & 0xffffu) | ((kBias - (ref >> 16)) << 16);
+            M = pk_add(M, dd);
+        }
         const Raw t = sa;
         sa = sb;
         sb = t;
     }
     // Steps past T: clear their survivor bits so that location 0 keeps its place there.
     for (int k = T >> 4; k < (Tpad >> 4); k++) {
-        const uint32_t keep = (k == (T >> 4)) ? ((1u << (T & 15)) - 1u) * 0x10001u : 0u;
+        uint32_t keep = 0;
+        if (k == (T >> 4)) {
+            for (int st = 0; st < (T & 15); st++) keep |= 0x00010001u << (8 * (st & 1) + 7 - (st >> 1));
+        }
         dec[k * 64 + lane] &= keep;
     }
     __syncthreads();
