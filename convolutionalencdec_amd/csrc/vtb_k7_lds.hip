@@ -65,6 +65,7 @@ using namespace k7;
 constexpr int kHalf = 24;     // table rows staged at a time (ring of 2 halves = kChunk rows)
 constexpr int kRowBytes = 32; // branch-metric table row: (V, W) of the four edge labels
 constexpr int kTbWarm = 48;   // traceback warm-up steps past a block's end
+constexpr uint32_t kBias1 = 4096;  // renormalised metrics: kBias1 +- 3060 (soft)
 
 int tb_block(int T) {
     const int per = (T + 31) / 32;  // 32 blocks per frame, multiple of 48 steps
@@ -116,7 +117,9 @@ __device__ __forceinline__ void acs_pair(uint32_t m, uint2 vw, uint32_t r, uint3
 }
 
 // Bit of step s (0..15) of a frame in its 16-bit half of a decision word (see the ACS).
-constexpr int word_bit(int s) { return 8 * (s & 1) + 7 - (s >> 1); }
+constexpr int word_bit(int s) {
+    return 8 * ((s >> 1) & 1) + 7 - (s & 1) - 2 * ((s >> 2) & 1) - 4 * ((s >> 3) & 1);
+}
 
 // 48 traceback steps over steps [tlo, tlo + 48) (tlo a multiple of 48), newest first, on
 // the lane index lam of the survivor's location.  Returns the 48 decoded bits (MSB = step
@@ -152,13 +155,18 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 // Measurement-only variants (tools/build_variants.sh builds them into separate libraries,
 // never the shipped one; their outputs are wrong): no table staging inside the ACS loop /
 // no survivor-word stores.
+#ifdef VTB_EXP_K15
+#define VTB_EXP_ODD(d) ((d) >> 1)
+#else
+#define VTB_EXP_ODD(d) (d)
+#endif
 #ifdef VTB_EXP_NO_STAGE
 #define VTB_EXP_STAGE false
 #else
 #define VTB_EXP_STAGE true
 #endif
 #ifdef VTB_EXP_NO_WORD
-#define VTB_EXP_WORD(x) asm volatile("" ::"v"(z), "v"(z_p))
+#define VTB_EXP_WORD(x) asm volatile("" ::"v"(r), "v"(r_p))
 #else
 #define VTB_EXP_WORD(x) x
 #endif
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
-    constexpr uint32_t INIT2 = 2 * (12 * Q + 1);  // doubled start metric of states != 0 (see header)
+    constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
     extern __shared__ uint4 smem4[];
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem4);
     uint8_t* tab = smem;
@@ -188,7 +196,13 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         for (int ph = 0; ph < 6; ph++) {
             const int p = 5 - ph;
             off[ph] = 8u * table.symm[rotl6(loc & ~(1 << p), ph)];
-            rr[ph] = uint32_t((loc >> p) & 1) * 0x10001u;
+            // A1 = A + R - 1 + 2^k: bit k of A1 - B is [A + R > B] (k = 15 on even, 14 on
+            // odd steps; |A + R - B| < 2^14 and A1 < 65536 keep both halves apart)
+#ifdef VTB_EXP_K15
+            rr[ph] = (uint32_t((loc >> p) & 1) + (1u << 15) - 1u) * 0x10001u;
+#else
+            rr[ph] = (uint32_t((loc >> p) & 1) + (1u << (15 - (ph & 1))) - 1u) * 0x10001u;
+#endif
         }
     }
 
@@ -231,13 +245,13 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         q0 &= keep;
         q1 &= keep;
         // doubled branch metrics of labels 0..3 (bit 0 of a label <-> coded bit 0):
-        // e0 = 2(q0+q1), e3 = 4Q - e0, e1 = 2(Q - q0 + q1), e2 = 2(Q + q0 - q1)
+        // e0 = q0+q1, e3 = 2Q - e0, e1 = Q - q0 + q1, e2 = Q + q0 - q1
         constexpr uint32_t R1 = 0x10001u;
-        const uint32_t e0 = (q0 + q1) << 1;
-        const uint32_t e3 = 4 * Q * R1 - e0;
+        const uint32_t e0 = q0 + q1;
+        const uint32_t e3 = 2 * Q * R1 - e0;
         const uint32_t dq = pk_sub(q1, q0);
-        const uint32_t e1 = pk_add(2 * Q * R1, pk_add(dq, dq));
-        const uint32_t e2 = pk_sub(2 * Q * R1, pk_add(dq, dq));
+        const uint32_t e1 = pk_add(Q * R1, dq);
+        const uint32_t e2 = pk_sub(Q * R1, dq);
         if (lane < kHalf) {
             uint4* row = reinterpret_cast<uint4*>(tab + ((h & 1) * kHalf + lrow) * kRowBytes);
             row[0] = make_uint4(e0, e3, e1, e2);  // (V, W) of labels c = 0, 1
@@ -245,7 +259,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         }
     };
 
-    uint32_t M = (lane == 0) ? kBias * 0x10001u : (kBias + INIT2) * 0x10001u;
+    uint32_t M = (lane == 0) ? kBias1 * 0x10001u : (kBias1 + INIT) * 0x10001u;
     Raw sa, sb;  // raw input of chunks c and c+1
     load_chunk(0, sa);
     stage_half(0, sa.a[0], sa.b[0]);
@@ -258,10 +272,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         nx1[k] = *reinterpret_cast<const uint2*>(tab + (6 + k) * kRowBytes + off[k]);
     }
 
-    // Decision words: the 32 sign bits of 16 steps are gathered by a tree -- v_perm of the
-    // sign bytes of two steps, then three levels of shift + bit-field insert -- into one
-    // word per lane: byte 2f + (s & 1), bit 7 - (s >> 1) holds step s of frame f.
-    uint32_t d_even = 0, x_p = 0, y_p = 0, z_p = 0;
+    // Decision words: the decision of an even step lands on bits 15/31 of d, of an odd step
+    // on bits 14/30 (rr); a tree -- bit-field insert of two steps, v_perm of the decision
+    // bytes of two pairs, two levels of shift + insert -- gathers the 32 bits of 16 steps
+    // into one word per lane (bit positions: word_bit()).
+    uint32_t d_even = 0, u_p = 0, p_p = 0, r_p = 0;
     const int tacs = (dbg & 2) ? 0 : Tpad;
     for (int t0 = 0; t0 < tacs; t0 += kChunk) {
         const int h0 = t0 / kHalf;  // half index of this chunk's first half
@@ -275,23 +290,23 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         uint32_t A, A1, B;                                                                           \
         acs_pair<5 - (PH)>(M, cur[PH], rr[PH], A, A1, B);                                            \
         M = pk_min(A, B);                                                                            \
-        const uint32_t d = pk_sub(B, A1); /* sign bits 15, 31: C = [A + R > B], frames A, B */       \
+        const uint32_t d = pk_sub(A1, B); /* bit k, 16 + k: C = [A + R > B] of frames A, B */       \
         if (((I) & 1) == 0) {                                                                        \
             d_even = d;                                                                              \
         } else {                                                                                     \
-            const uint32_t x = __builtin_amdgcn_perm(d, d_even, 0x07030501u);                        \
+            const uint32_t u = bfi(0x80008000u, d_even, VTB_EXP_ODD(d)); /* bits 15, 14 of each half */ \
             if (((I) & 3) == 1) {                                                                    \
-                x_p = x;                                                                             \
+                u_p = u;                                                                             \
             } else {                                                                                 \
-                const uint32_t y = bfi(0x80808080u, x_p, x >> 1);                                    \
+                const uint32_t pq = __builtin_amdgcn_perm(u, u_p, 0x07030501u);                      \
                 if (((I) & 7) == 3) {                                                                \
-                    y_p = y;                                                                         \
+                    p_p = pq;                                                                        \
                 } else {                                                                             \
-                    const uint32_t z = bfi(0xC0C0C0C0u, y_p, y >> 2);                                \
+                    const uint32_t r = bfi(0xC0C0C0C0u, p_p, pq >> 2);                               \
                     if (((I) & 15) == 7) {                                                           \
-                        z_p = z;                                                                     \
+                        r_p = r;                                                                     \
                     } else {                                                                         \
-                        VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = bfi(0xF0F0F0F0u, z_p, z >> 4));       \
+                        VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = bfi(0xF0F0F0F0u, r_p, r >> 4));       \
                     }                                                                                \
                 }                                                                                    \
             }                                                                                        \
@@ -317,11 +332,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
-        // renormalise once per chunk: 48 steps add at most 48 * 1020 to a doubled metric, so
-        // values stay below kBias + 6120 + 48960 < 65536
+        // renormalise once per chunk: 48 steps add at most 48 * 510 to a metric, so values
+        // stay below kBias1 + 3061 + 3060 + 24480 (+ 2^15 in A1) < 65536
         {
             const uint32_t ref = __builtin_amdgcn_readlane(M, 0);
-            const uint32_t dd = ((kBias - (ref & 0xffffu)) & 0xffffu) | ((kBias - (ref >> 16)) << 16);
+            const uint32_t dd = ((kBias1 - (ref & 0xffffu)) & 0xffffu) | ((kBias1 - (ref >> 16)) << 16);
             M = pk_add(M, dd);
         }
         const Raw t = sa;
@@ -332,7 +347,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     for (int k = T >> 4; k < (Tpad >> 4); k++) {
         uint32_t keep = 0;
         if (k == (T >> 4)) {
-            for (int st = 0; st < (T & 15); st++) keep |= 0x00010001u << (8 * (st & 1) + 7 - (st >> 1));
+            for (int st = 0; st < (T & 15); st++) keep |= 0x00010001u << word_bit(st);
         }
         dec[k * 64 + lane] &= keep;
     }
