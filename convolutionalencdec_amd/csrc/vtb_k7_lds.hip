@@ -17,43 +17,57 @@
 // quad_perm, row_half_mirror, row_ror:8 (folded into the add), in-place
 // v_permlane16_swap, v_permlane32_swap.
 //
-// Branch metrics: a ring of 48 table rows in LDS, staged 24 steps at a time by 24 lanes
-// (vtb_k7_common.h write_row): per step eight (V, W) pairs, V = 2e(c) + R, W = 2e(~c).
-// Lane l reads its pair with one ds_read_b64 at a per-phase offset (its label c, and
-// R = bit p of l), one group of six steps ahead.  The ACS step is
-//     A = M + V;  B = partner(M) + W;  M' = min(A, B) & ~1;  d = B - A
-// Metrics are doubled so that the R bit added to the own-path candidate of lanes whose
-// own state is the upper predecessor j+32 turns "A > B" into "A >= B" for exactly those
-// lanes: the sign of d (per 16-bit half) is C = [A > B], and the reference's decision
-// (strict '>' toward the lower predecessor j, viterbiDecoderButterflyk1.c:129-130) is
-// D = C xor R.  The and clears the R bit again.
+// Metrics carry their decisions.  A stored metric is 4m + h: the exact integer path
+// metric m (renormalised) times four, plus two low "history" bits h.  Step t puts a tie
+// bit at position b = t & 1 into both candidates: the own candidate gets R << b and the
+// partner's (1 - R) << b, where R = bit p of the lane's location (R = 1: the lane's own
+// state is the upper predecessor j+32).  So the two candidates never compare equal, an
+// exact tie goes to the lower predecessor j as in the reference (strict '>',
+// viterbiDecoderButterflyk1.c:129-130), and bit b of the minimum is the decision
+// D = R xor [partner won] = the location bit p of the survivor's predecessor.  The ACS is
+// three instructions per step for two frames:
+//     A = M + V;  B = partner(M) + W;  M' = pk_min(A, B)
+// with (V, W) = (4e(c) + R << b, 4e(~c) + (1 - R) << b) read from a branch-metric table
+// row in LDS (c = the butterfly's edge label).  History bits below b never reach a
+// comparison's outcome (candidate metrics differ by multiples of 4).  After the odd step
+// of each two-step window the history holds [D_odd at this location, D_even at the
+// survivor's predecessor] -- exactly the two decisions a traceback through this location
+// reads -- so the two bits are appended to the lane's survivor word and cleared.
+//
+// Table rows (one per step): eight (V, W) u32 pairs for (c, R), both frames packed, staged
+// for a whole 48-step chunk at a time by 48 lanes from raw input bytes loaded a chunk
+// earlier, into a 48-row LDS ring stored column-major: pair k of ring row r at 8-byte slot
+// 49k + r.  Staging writes (lane = row) are then contiguous ds_write_b64s and the eight
+// pairs of one row sit in distinct banks for the broadcast ds_read_b64 of a step.  Steps past T (padding up to the chunk size) use
+// rows V = tie, W = 4(12Q + 1) + tie that make every lane keep its own predecessor, so
+// the survivor at location 0 stays at location 0 through the padding.
 //
 // Initial metrics: the reference starts state 0 at 0 and every other state at
 // (uint8)(N+1) = 65 (x255 soft).  For K=7 any start value above 12Q (six steps of the
 // largest branch metric) yields the same decisions -- during the first six steps a path
 // from state 0 always beats one from another state, paths from other states compare
 // with equal offsets, and from step 6 on every state descends from state 0 -- so this
-// kernel uses 12Q + 1, which keeps all candidate differences far inside int16.
+// kernel uses 12Q + 1.
 //
-// Renormalisation every 16 steps (subtract location 0's metric, add a bias) replaces the
+// Renormalisation every 12 steps (subtract location 0's metric taken at the start of the
+// window, add a bias) folds into the history clear as one v_xad_u32; it replaces the
 // reference's uint8 renorm (exact metrics have a bounded spread).
 //
-// Survivors.  The sign bits of d accumulate in one VGPR per lane, frame A in bits 0..15
-// and frame B in bits 16..31 (bit j = step 16k + j), and every 16 steps the wave writes
-// its 64 words (256 B, one ds_write_b32) to LDS.  No scalar stores, no VALU lane writes.
+// Survivors.  Each lane appends its two history bits per window to one VGPR (frame A in
+// bits 0..15, frame B in bits 16..31, oldest window highest) and every 16 steps the wave
+// writes its 64 words (256 B, one ds_write_b32) to LDS.
 //
-// Traceback (reference :200-256), in location space: going back from step t+1 to t the
-// decoded bit is bit p_t of the location and the location's bit p_t becomes D_t[loc],
-// i.e. loc ^= C_t[loc] << p_t.  Within a sextet p runs 0..5, so a sextet's six decoded
-// bits are the location at its start, MSB first.  Lanes 0-31 trace blocks of frame A,
-// lanes 32-63 of frame B, each block of TBB steps (a multiple of 48) walking back from
-// 48 steps past its end as a chain of dependent LDS reads.  A block whose walk starts at
-// or beyond T starts at the known location 0 (the terminated path ends in state 0; the
-// survivor words of steps past T are cleared so location 0 stays put).  Every other
-// block starts at a guess and is verified: its location on entering the block must equal
-// the location its successor ended on; a block that disagrees is re-walked from its
-// successor's proven location.  So the output is exactly the reference's for every
-// input; only the time depends on how fast survivor paths merge.
+// Traceback (reference :200-256), in location space, two steps per LDS read: from the
+// location at the end of a window, the word's two bits are the new location bits p_odd
+// and then p_even.  A sextet's six decoded bits are the location at its end (MSB = the
+// oldest step).  Lanes 0-31 trace blocks of frame A, lanes 32-63 of frame B, each block
+// of TBB steps (a multiple of 48) walking back from 48 steps past its end as a chain of
+// dependent LDS reads.  A block whose walk starts at or beyond T starts at the known
+// location 0 (the terminated path ends in state 0).  Every other block starts at a guess
+// and is verified: its location on entering the block must equal the location its
+// successor ended on; a block that disagrees is re-walked from its successor's proven
+// location.  So the output is exactly the reference's for every input; only the time
+// depends on how fast survivor paths merge.
 
 #include "vtb_k7_common.h"
 
@@ -62,10 +76,12 @@ namespace {
 
 using namespace k7;
 
-constexpr int kHalf = 24;     // table rows staged at a time (ring of 2 halves = kChunk rows)
-constexpr int kRowBytes = 32; // branch-metric table row: (V, W) of the four edge labels
-constexpr int kTbWarm = 48;   // traceback warm-up steps past a block's end
-constexpr uint32_t kBias1 = 4096;  // renormalised metrics: kBias1 +- 3060 (soft)
+constexpr int kCol = 49;                   // 8-byte slots per table column (48 rows + bank skew)
+constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) columns
+constexpr int kTbWarm = 48;    // traceback warm-up steps past a block's end
+constexpr uint32_t kR1 = 0x10001u;
+constexpr uint32_t kHist = 0x00030003u;  // history bits of both frames
+constexpr uint32_t kBias4 = 4 * 3060;    // renormalised metric of location 0, times four
 
 int tb_block(int T) {
     const int per = (T + 31) / 32;  // 32 blocks per frame, multiple of 48 steps
@@ -74,71 +90,52 @@ int tb_block(int T) {
 int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
-int region0(int T) { return 8 * tb_block(T) > kChunk * kRowBytes ? 8 * tb_block(T) : kChunk * kRowBytes; }
+int region0(int T) { return 8 * tb_block(T) > kRingBytes ? 8 * tb_block(T) : kRingBytes; }
 size_t lds_bytes(int T) { return (size_t)region0(T) + 16 * (size_t)t_pad(T); }
 
 // lane <-> location map (an involution)
-__device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ (((l >> 2) & 1u) * 3u); }
+__host__ __device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ (((l >> 2) & 1u) * 3u); }
 
-// Partner metric across location bit P, plus w (lane XOR 1, 2, 7, 8, 16, 32).
+// The candidates of a step: A = own metric + V, B = partner's metric (across location bit
+// P: lane XOR 1, 2, 7, 8, 16, 32) + W.  For the permlane phases the add of A separates the
+// last VALU write of m from the swap and an s_nop separates the swap from the read of its
+// result (one wait state each way: tools/probes/permlane_hazard.hip).
 template <int P>
-__device__ __forceinline__ uint32_t exch_plus(uint32_t m, uint32_t w) {
-    if constexpr (P == 2) {
-        return __builtin_amdgcn_update_dpp(0u, m, 0x141, 0xF, 0xF, true) + w;  // row_half_mirror: XOR 7
-    } else {
-        return partner_plus<P>(m, w);
-    }
-}
-
-__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (a & mask) | (b & ~mask); }
-
-// The candidates of a step: A = own metric + V, B = partner's metric + W, and A1 = A + R
-// (R = 1 in both halves for lanes whose own state is the upper predecessor), so that
-// [A1 > B] is the reference's decision rule for either lane of a butterfly.  For the
-// permlane phases the add of A separates the last write of M from the swap and the add of
-// A1 separates the swap from the read of its result, inside one asm block (the swap needs
-// one wait state after a VALU write of its operand: permlane_hazard probe).
-template <int P>
-__device__ __forceinline__ void acs_pair(uint32_t m, uint2 vw, uint32_t r, uint32_t& A, uint32_t& A1, uint32_t& B) {
+__device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, uint32_t& B) {
     if constexpr (P == 4 || P == 5) {
         if constexpr (P == 4) {
-            asm volatile("v_add_u32 %0, %2, %3\n\tv_permlane16_swap_b32 %2, %2\n\tv_add_u32 %1, %0, %4"
-                         : "=&v"(A), "=&v"(A1), "+v"(m) : "v"(vw.x), "v"(r));
+            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
+                         : "=&v"(A), "+v"(m) : "v"(vw.x));
         } else {
-            asm volatile("v_add_u32 %0, %2, %3\n\tv_permlane32_swap_b32 %2, %2\n\tv_add_u32 %1, %0, %4"
-                         : "=&v"(A), "=&v"(A1), "+v"(m) : "v"(vw.x), "v"(r));
+            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 0"
+                         : "=&v"(A), "+v"(m) : "v"(vw.x));
         }
         B = m + vw.y;
     } else {
         A = m + vw.x;
-        A1 = A + r;
-        B = exch_plus<P>(m, vw.y);
+        if constexpr (P == 2) {
+            B = __builtin_amdgcn_update_dpp(0u, m, 0x141, 0xF, 0xF, true) + vw.y;  // row_half_mirror: XOR 7
+        } else {
+            B = partner_plus<P>(m, vw.y);
+        }
     }
 }
 
-// Bit of step s (0..15) of a frame in its 16-bit half of a decision word (see the ACS).
-constexpr int word_bit(int s) {
-    return 8 * ((s >> 1) & 1) + 7 - (s & 1) - 2 * ((s >> 2) & 1) - 4 * ((s >> 3) & 1);
-}
-
-// 48 traceback steps over steps [tlo, tlo + 48) (tlo a multiple of 48), newest first, on
-// the lane index lam of the survivor's location.  Returns the 48 decoded bits (MSB = step
-// tlo): each sextet's bits are its starting location.
-__device__ __forceinline__ uint64_t tb_body(const uint8_t* decf, int tlo, uint32_t& lam) {
+// 48 traceback steps over [tlo, tlo + 48) (tlo a multiple of 48), newest first, in
+// location space.  Returns the 48 decoded bits (MSB = step tlo).
+__device__ __forceinline__ uint64_t tb_body(const uint8_t* decf, int tlo, uint32_t& loc) {
     const uint8_t* base = decf + (tlo >> 4) * 256;
     uint64_t bits = 0;
 #pragma unroll
-    for (int j = 0; j < 48; j++) {
-        const int s = word_bit((47 - j) & 15);  // bit of step t = tlo + 47 - j in its half-word
-        const int p = j % 6;          // pairing bit of that step
-        if (p == 0) bits |= uint64_t(lane_of(lam)) << (6 * (j / 6));
-        const uint32_t w = *reinterpret_cast<const unsigned short*>(base + ((47 - j) >> 4) * 256 + lam * 4);
-        if (p == 2) {
-            lam ^= uint32_t(int32_t(w << (31 - s)) >> 31) & 7u;  // C ? XOR 7
-        } else {
-            const uint32_t x = s >= p ? (w >> (s - p)) : (w << (p - s));
-            lam ^= x & (1u << p);
-        }
+    for (int j = 0; j < 24; j++) {
+        const int todd = 47 - 2 * j;  // odd step of the window, relative to tlo
+        if (j % 3 == 0) bits |= uint64_t(loc) << (6 * (j / 3));  // sextet boundary tlo + todd + 1
+        const int sh = 14 - 2 * ((todd & 15) >> 1);                // window's bits in its half-word
+        const uint32_t v =
+            *reinterpret_cast<const unsigned short*>(base + (todd >> 4) * 256 + lane_of(loc) * 4);
+        const int p1 = 5 - todd % 6, p0 = 5 - (todd - 1) % 6;
+        loc = (loc & ~(1u << p1)) | (((v >> (sh + 1)) & 1u) << p1);
+        loc = (loc & ~(1u << p0)) | (((v >> sh) & 1u) << p0);
     }
     return bits;
 }
@@ -155,18 +152,13 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 // Measurement-only variants (tools/build_variants.sh builds them into separate libraries,
 // never the shipped one; their outputs are wrong): no table staging inside the ACS loop /
 // no survivor-word stores.
-#ifdef VTB_EXP_K15
-#define VTB_EXP_ODD(d) ((d) >> 1)
-#else
-#define VTB_EXP_ODD(d) (d)
-#endif
 #ifdef VTB_EXP_NO_STAGE
 #define VTB_EXP_STAGE false
 #else
 #define VTB_EXP_STAGE true
 #endif
 #ifdef VTB_EXP_NO_WORD
-#define VTB_EXP_WORD(x) asm volatile("" ::"v"(r), "v"(r_p))
+#define VTB_EXP_WORD(x) asm volatile("" ::"v"(acc))
 #else
 #define VTB_EXP_WORD(x) x
 #endif
@@ -185,143 +177,122 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const size_t fa = (size_t)blockIdx.x * 2, fb = fa + 1;
     const bool has_b = fb < frames;
     const uint8_t* inA = in + fa * in_stride;
-    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;
+    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
 
-    // Per phase: byte offset of the lane's (V, W) pair in a table row (its edge label c) and
-    // the tie bit R (bit p of the lane's location), packed for both frames.
-    uint32_t off[6], rr[6];
+    // Per phase: byte offset of the lane's (V, W) column in the table ring: its edge label c
+    // and R = bit p of its location.
+    uint32_t off[6];
     {
         const int loc = int(lane_of(lane));
 #pragma unroll
         for (int ph = 0; ph < 6; ph++) {
             const int p = 5 - ph;
-            off[ph] = 8u * table.symm[rotl6(loc & ~(1 << p), ph)];
-            // A1 = A + R - 1 + 2^k: bit k of A1 - B is [A + R > B] (k = 15 on even, 14 on
-            // odd steps; |A + R - B| < 2^14 and A1 < 65536 keep both halves apart)
-#ifdef VTB_EXP_K15
-            rr[ph] = (uint32_t((loc >> p) & 1) + (1u << 15) - 1u) * 0x10001u;
-#else
-            rr[ph] = (uint32_t((loc >> p) & 1) + (1u << (15 - (ph & 1))) - 1u) * 0x10001u;
-#endif
+            off[ph] = 8u * kCol * (table.symm[rotl6(loc & ~(1 << p), ph)] + 4u * ((loc >> p) & 1u));
         }
     }
 
-    // Table staging.  Lane r < 24 builds the rows of steps 24k + r.  The raw input bytes of
-    // a chunk (48 steps: both halves, both frames) are loaded a whole chunk ahead into one of
-    // two register sets and first touched (behind an empty asm, so the compiler cannot
-    // hoist the byte unpacking next to the load) when a half is staged, 48-72 steps later.
-    const int lrow = lane % kHalf;
-    struct Raw {
-        uint32_t a[2], b[2];  // [half]: frame A / B bytes of step t (soft q0 | q1 << 8, hard the byte)
-    };
-    auto load_chunk = [&](int c, Raw& r) {
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int t = c * kChunk + k * kHalf + lrow;
-            const int tc = t < T ? t : T - 1;
-            if constexpr (SOFT) {
-                unsigned short x, y;
-                __builtin_memcpy(&x, inA + 2 * (size_t)tc, 2);
-                __builtin_memcpy(&y, inB + 2 * (size_t)tc, 2);
-                r.a[k] = x;
-                r.b[k] = y;
-            } else {
-                r.a[k] = inA[tc];
-                r.b[k] = inB[tc];
-            }
+    // Table staging: lane r < 48 builds the row of step 48c + r from the raw input bytes of
+    // that step (soft q0 | q1 << 8, hard the byte), loaded one chunk earlier and first
+    // touched (behind an empty asm, so the compiler cannot hoist the unpacking next to the
+    // load) when the chunk is staged.
+    auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
+        const int t = c * kChunk + (lane < kChunk ? lane : 0);
+        const int tc = t < T ? t : T - 1;
+        if constexpr (SOFT) {
+            unsigned short x, y;
+            __builtin_memcpy(&x, inA + 2 * (size_t)tc, 2);
+            __builtin_memcpy(&y, inB + 2 * (size_t)tc, 2);
+            ra = x;
+            rb = y;
+        } else {
+            ra = inA[tc];
+            rb = inB[tc];
         }
     };
-    auto stage_half = [&](int h, uint32_t ra, uint32_t rb) {
+    auto stage = [&](int c, uint32_t ra, uint32_t rb) {
         asm volatile("" : "+v"(ra), "+v"(rb));
-        const int t = h * kHalf + lrow;
-        // packed [frame A, frame B] received values of coded bits 0 and 1
+        // packed [frame A, frame B] received values of coded bits 0 and 1, times four
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
         uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
         if constexpr (!SOFT) {
-            q1 = (q0 >> 1) & 0x00010001u;
-            q0 &= 0x00010001u;
+            q1 = (q0 >> 1) & kR1;
+            q0 &= kR1;
         }
-        const uint32_t keep = (t < T ? 0x0000FFFFu : 0u) | ((t < T && has_b) ? 0xFFFF0000u : 0u);
-        q0 &= keep;
-        q1 &= keep;
-        // doubled branch metrics of labels 0..3 (bit 0 of a label <-> coded bit 0):
-        // e0 = q0+q1, e3 = 2Q - e0, e1 = Q - q0 + q1, e2 = Q + q0 - q1
-        constexpr uint32_t R1 = 0x10001u;
-        const uint32_t e0 = q0 + q1;
-        const uint32_t e3 = 2 * Q * R1 - e0;
-        const uint32_t dq = pk_sub(q1, q0);
-        const uint32_t e1 = pk_add(Q * R1, dq);
-        const uint32_t e2 = pk_sub(Q * R1, dq);
-        if (lane < kHalf) {
-            uint4* row = reinterpret_cast<uint4*>(tab + ((h & 1) * kHalf + lrow) * kRowBytes);
-            row[0] = make_uint4(e0, e3, e1, e2);  // (V, W) of labels c = 0, 1
-            row[1] = make_uint4(e2, e1, e3, e0);  // (V, W) of labels c = 2, 3
+        q0 <<= 2;
+        q1 <<= 2;
+        // 4e of labels 0..3 (bit 0 of a label <-> coded bit 0); halves never borrow
+        constexpr uint32_t QQ = 4 * Q * kR1;
+        const uint32_t e0 = q0 + q1, e1 = (QQ + q1) - q0, e2 = 2 * QQ - e1, e3 = 2 * QQ - e0;
+        uint32_t v0 = e0, v1 = e1, v2 = e2, v3 = e3, w0 = e0, w1 = e1, w2 = e2, w3 = e3;
+        if ((c + 1) * kChunk > T) {  // chunk reaches past T: padding rows (wave-uniform branch)
+            const bool pad = c * kChunk + lane >= T;
+            constexpr uint32_t PADW = 4 * (12 * Q + 1) * kR1;
+            if (pad) {
+                v0 = v1 = v2 = v3 = 0;
+                w0 = w1 = w2 = w3 = PADW;
+            }
+        }
+        const uint32_t tie = (1u + (lane & 1)) * kR1;  // bit b = t & 1 of both halves
+        if (lane < kChunk) {
+            uint2* col = reinterpret_cast<uint2*>(tab) + lane;  // column k at col[kCol * k]
+            col[0 * kCol] = make_uint2(v0, w3 + tie);  // (c, R = 0)
+            col[1 * kCol] = make_uint2(v1, w2 + tie);
+            col[2 * kCol] = make_uint2(v2, w1 + tie);
+            col[3 * kCol] = make_uint2(v3, w0 + tie);
+            col[4 * kCol] = make_uint2(v0 + tie, w3);  // (c, R = 1)
+            col[5 * kCol] = make_uint2(v1 + tie, w2);
+            col[6 * kCol] = make_uint2(v2 + tie, w1);
+            col[7 * kCol] = make_uint2(v3 + tie, w0);
         }
     };
 
-    uint32_t M = (lane == 0) ? kBias1 * 0x10001u : (kBias1 + INIT) * 0x10001u;
-    Raw sa, sb;  // raw input of chunks c and c+1
-    load_chunk(0, sa);
-    stage_half(0, sa.a[0], sa.b[0]);
-    load_chunk(1, sb);
+    uint32_t M = (lane == 0) ? kBias4 * kR1 : (kBias4 + 4 * INIT) * kR1;
+    uint32_t ra, rb;
+    load_raw(0, ra, rb);
+    stage(0, ra, rb);
+    load_raw(1, ra, rb);
     // software pipeline: the table pairs of group G+2 are read while group G computes
     uint2 cur[6], nx1[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-        cur[k] = *reinterpret_cast<const uint2*>(tab + k * kRowBytes + off[k]);
-        nx1[k] = *reinterpret_cast<const uint2*>(tab + (6 + k) * kRowBytes + off[k]);
+        cur[k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * k);
+        nx1[k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * (6 + k));
     }
 
-    // Decision words: the decision of an even step lands on bits 15/31 of d, of an odd step
-    // on bits 14/30 (rr); a tree -- bit-field insert of two steps, v_perm of the decision
-    // bytes of two pairs, two levels of shift + insert -- gathers the 32 bits of 16 steps
-    // into one word per lane (bit positions: word_bit()).
-    uint32_t d_even = 0, u_p = 0, p_p = 0, r_p = 0;
+    uint32_t acc = 0, dd = 0;
     const int tacs = (dbg & 2) ? 0 : Tpad;
     for (int t0 = 0; t0 < tacs; t0 += kChunk) {
-        const int h0 = t0 / kHalf;  // half index of this chunk's first half
+        const int c0 = t0 / kChunk;
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
         uint32_t* dchunk = dec + (t0 >> 4) * 64 + lane;
 
-#define VTB_STEP(I, PH)                                                                              \
-    {                                                                                                \
-        uint32_t A, A1, B;                                                                           \
-        acs_pair<5 - (PH)>(M, cur[PH], rr[PH], A, A1, B);                                            \
-        M = pk_min(A, B);                                                                            \
-        const uint32_t d = pk_sub(A1, B); /* bit k, 16 + k: C = [A + R > B] of frames A, B */       \
-        if (((I) & 1) == 0) {                                                                        \
-            d_even = d;                                                                              \
-        } else {                                                                                     \
-            const uint32_t u = bfi(0x80008000u, d_even, VTB_EXP_ODD(d)); /* bits 15, 14 of each half */ \
-            if (((I) & 3) == 1) {                                                                    \
-                u_p = u;                                                                             \
-            } else {                                                                                 \
-                const uint32_t pq = __builtin_amdgcn_perm(u, u_p, 0x07030501u);                      \
-                if (((I) & 7) == 3) {                                                                \
-                    p_p = pq;                                                                        \
-                } else {                                                                             \
-                    const uint32_t r = bfi(0xC0C0C0C0u, p_p, pq >> 2);                               \
-                    if (((I) & 15) == 7) {                                                           \
-                        r_p = r;                                                                     \
-                    } else {                                                                         \
-                        VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = bfi(0xF0F0F0F0u, r_p, r >> 4));       \
-                    }                                                                                \
-                }                                                                                    \
-            }                                                                                        \
-        }                                                                                            \
+#define VTB_STEP(I, PH)                                                                          \
+    {                                                                                            \
+        if (((I) % 12) == 10) {                                                                  \
+            /* renormalisation reference: location 0 (lane 0), history clear at this point */    \
+            dd = kBias4 * kR1 - __builtin_amdgcn_readfirstlane(M);                                \
+        }                                                                                        \
+        uint32_t A, B;                                                                           \
+        candidates<5 - (PH)>(M, cur[PH], A, B);                                                  \
+        M = pk_min(A, B);                                                                        \
+        if ((I) & 1) {                                                                           \
+            const uint32_t x = M & kHist;                                                        \
+            M = (((I) % 12) == 11) ? ((M ^ x) + dd) : (M ^ x);                                   \
+            acc = (((I) & 15) == 1) ? x : ((acc << 2) | x);                                      \
+            if (((I) & 15) == 15) VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = acc);                   \
+        }                                                                                        \
     }
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
         uint2 nx2[6];                                                                             \
         _Pragma("unroll") for (int k = 0; k < 6; k++) nx2[k] =                                    \
-            ap[k][((6 * ((G) + 2) + k) % kChunk) * (kRowBytes / 8)];                              \
-        if ((G) == 1 && VTB_EXP_STAGE) {                                                          \
-            stage_half(h0 + 1, sa.a[1], sa.b[1]);                                                 \
-            load_chunk(h0 / 2 + 2, sa);                                                           \
+            ap[k][(6 * ((G) + 2) + k) % kChunk];                              \
+        if ((G) == 5 && VTB_EXP_STAGE) {                                                          \
+            stage(c0 + 1, ra, rb);                                                                \
+            load_raw(c0 + 2, ra, rb);                                                             \
         }                                                                                         \
-        if ((G) == 5 && VTB_EXP_STAGE) stage_half(h0 + 2, sb.a[0], sb.b[0]);                      \
         VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1) VTB_STEP(6 * (G) + 2, 2)                \
         VTB_STEP(6 * (G) + 3, 3) VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                \
         _Pragma("unroll") for (int k = 0; k < 6; k++) {                                           \
@@ -332,24 +303,6 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
-        // renormalise once per chunk: 48 steps add at most 48 * 510 to a metric, so values
-        // stay below kBias1 + 3061 + 3060 + 24480 (+ 2^15 in A1) < 65536
-        {
-            const uint32_t ref = __builtin_amdgcn_readlane(M, 0);
-            const uint32_t dd = ((kBias1 - (ref & 0xffffu)) & 0xffffu) | ((kBias1 - (ref >> 16)) << 16);
-            M = pk_add(M, dd);
-        }
-        const Raw t = sa;
-        sa = sb;
-        sb = t;
-    }
-    // Steps past T: clear their survivor bits so that location 0 keeps its place there.
-    for (int k = T >> 4; k < (Tpad >> 4); k++) {
-        uint32_t keep = 0;
-        if (k == (T >> 4)) {
-            for (int st = 0; st < (T & 15); st++) keep |= 0x00010001u << word_bit(st);
-        }
-        dec[k * 64 + lane] &= keep;
     }
     __syncthreads();
     if (dbg & 1) return;
@@ -363,30 +316,30 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const int start = min(start_full, Tpad);
     const bool known = start >= T;  // walk starts on the known path (location 0 at and past T)
     const int nbody = (kTbWarm + tbb) / 48;
-    uint32_t lam = 0, lam_top = 0;
+    uint32_t loc = 0, loc_top = 0;
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
-        if (g == kTbWarm / 48) lam_top = lam;
+        if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {  // lane's walk has begun (start is a multiple of 48)
-            const uint64_t bits = tb_body(decf, tlo, lam);
+            const uint64_t bits = tb_body(decf, tlo, loc);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
-    uint32_t fin = lam;  // survivor's lane index at step blk * tbb
+    uint32_t fin = loc;  // survivor's location at step blk * tbb
     bool ok = known;
     for (int round = 0; round < 32; round++) {
         if (!__any(!ok)) break;
         const uint32_t sf = __shfl_down(fin, 1);
         const int sok = __shfl_down(ok ? 1 : 0, 1);
         const bool cand = !ok && sok;
-        if (cand && lam_top == sf) ok = true;  // entered the block on the proven path
+        if (cand && loc_top == sf) ok = true;  // entered the block on the proven path
         if (cand && !ok) {
-            lam = sf;
+            loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb_body(decf, tlo, lam));
+                put_bits48(ob, tlo, tb_body(decf, tlo, loc));
             }
-            fin = lam;
+            fin = loc;
             ok = true;
         }
     }
