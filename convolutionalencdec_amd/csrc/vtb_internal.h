@@ -27,7 +27,8 @@ struct Launch {
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
-// Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS).  Never
+// Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
+// kernel: bit 2 skip traceback verification, bit 3 warm-up walk only).  Never
 // set in production; outputs are garbage when set.
 inline int debug_flags() {
     const char* v = getenv("VTB_DEBUG");

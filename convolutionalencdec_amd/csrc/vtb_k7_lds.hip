@@ -78,7 +78,10 @@ using namespace k7;
 
 constexpr int kCol = 49;                   // 8-byte slots per table column (48 rows + bank skew)
 constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) columns
-constexpr int kTbWarm = 48;    // traceback warm-up steps past a block's end
+#ifndef VTB_EXP_TBWARM
+#define VTB_EXP_TBWARM 48
+#endif
+constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
 constexpr uint32_t kR1 = 0x10001u;
 constexpr uint32_t kHist = 0x00030003u;  // history bits of both frames
 constexpr uint32_t kBias4 = 4 * 3060;    // renormalised metric of location 0, times four
@@ -90,7 +93,10 @@ int tb_block(int T) {
 int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
-int region0(int T) { return 8 * tb_block(T) > kRingBytes ? 8 * tb_block(T) : kRingBytes; }
+int region0(int T) {  // multiple of 256: the traceback edits survivor-word addresses in place
+    const int r = 8 * tb_block(T) > kRingBytes ? 8 * tb_block(T) : kRingBytes;
+    return (r + 255) / 256 * 256;
+}
 size_t lds_bytes(int T) { return (size_t)region0(T) + 16 * (size_t)t_pad(T); }
 
 // lane <-> location map (an involution)
@@ -121,32 +127,45 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     }
 }
 
-// 48 traceback steps over [tlo, tlo + 48) (tlo a multiple of 48), newest first, in
-// location space.  Returns the 48 decoded bits (MSB = step tlo).
-__device__ __forceinline__ uint64_t tb_body(const uint8_t* decf, int tlo, uint32_t& loc) {
-    const uint8_t* base = decf + (tlo >> 4) * 256;
+// Reversed location numbering for the survivor words and the traceback: l' = rev6(l), so
+// step t's pairing bit is bit t mod 6 of l' and a window's two decisions (even step at
+// the lower history bit) land on the adjacent bits (t_even mod 6, t_odd mod 6) of l'.
+__host__ __device__ __forceinline__ uint32_t rev6(uint32_t l) {
+    return ((l & 1) << 5) | ((l & 2) << 3) | ((l & 4) << 1) | ((l & 8) >> 1) | ((l & 16) >> 3) | ((l & 32) >> 5);
+}
+
+// 48 traceback steps over [tlo, tlo + 48) (tlo a multiple of 48), newest first.  cb is the
+// LDS byte address of the block's first survivor-word column (dec + 256 (tlo / 16) + 2f:
+// bits 2..7 clear) and l4 = 4 l' of the survivor's location, so cb | l4 addresses its word
+// and each window is one read, one shift and one bit-field insert on the address.
+// Returns the 48 decoded bits with bit 0 = step tlo (a sextet's bits are its end location
+// in l' numbering, oldest step at bit 0).
+__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4) {
+    uint32_t a = cb | l4;
     uint64_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 24; j++) {
         const int todd = 47 - 2 * j;  // odd step of the window, relative to tlo
-        if (j % 3 == 0) bits |= uint64_t(loc) << (6 * (j / 3));  // sextet boundary tlo + todd + 1
-        const int sh = 14 - 2 * ((todd & 15) >> 1);                // window's bits in its half-word
-        const uint32_t v =
-            *reinterpret_cast<const unsigned short*>(base + (todd >> 4) * 256 + lane_of(loc) * 4);
-        const int p1 = 5 - todd % 6, p0 = 5 - (todd - 1) % 6;
-        loc = (loc & ~(1u << p1)) | (((v >> (sh + 1)) & 1u) << p1);
-        loc = (loc & ~(1u << p0)) | (((v >> sh) & 1u) << p0);
+        if (j % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - j / 3));  // sextet end tlo + todd + 1
+        const int sh = 14 - 2 * ((todd & 15) >> 1);                           // window's bits in its half-word
+        uint32_t v;  // survivor half-word (smem is LDS address 0: dynamic LDS only)
+        asm volatile("ds_read_u16 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"((todd >> 4) * 256));
+        const int pos = 2 + (todd - 1) % 6;  // address bit of l' bit (t_even mod 6)
+        const uint32_t fld = pos >= sh ? (v << (pos - sh)) : (v >> (sh - pos));
+        a = (a & ~(3u << pos)) | (fld & (3u << pos));
     }
+    l4 = a & 0xFCu;
     return bits;
 }
 
+// Output bytes of steps [tlo, tlo + 48) (bit 0 of bits = step tlo; bytes MSB-first as the
+// reference packs them, viterbiDecoderButterflyk1.c:243-249).
 __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) {
     unsigned short* o = reinterpret_cast<unsigned short*>(ob + (tlo >> 3));
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const uint32_t hi = uint32_t(bits >> (40 - 16 * k)) & 0xffu, lo = uint32_t(bits >> (32 - 16 * k)) & 0xffu;
-        o[k] = (unsigned short)(hi | (lo << 8));
-    }
+    const uint32_t r = __builtin_bitreverse32(uint32_t(bits)), rh = __builtin_bitreverse32(uint32_t(bits >> 32));
+    o[0] = (unsigned short)((r >> 24) | ((r >> 8) & 0xff00u));
+    o[1] = (unsigned short)(((r >> 8) & 0xffu) | ((r & 0xffu) << 8));
+    o[2] = (unsigned short)((rh >> 24) | ((rh >> 8) & 0xff00u));
 }
 
 // Measurement-only variants (tools/build_variants.sh builds them into separate libraries,
@@ -225,12 +244,10 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         const uint32_t e0 = q0 + q1, e1 = (QQ + q1) - q0, e2 = 2 * QQ - e1, e3 = 2 * QQ - e0;
         uint32_t v0 = e0, v1 = e1, v2 = e2, v3 = e3, w0 = e0, w1 = e1, w2 = e2, w3 = e3;
         if ((c + 1) * kChunk > T) {  // chunk reaches past T: padding rows (wave-uniform branch)
-            const bool pad = c * kChunk + lane >= T;
+            const uint32_t keep = c * kChunk + lane < T ? ~0u : 0u;
             constexpr uint32_t PADW = 4 * (12 * Q + 1) * kR1;
-            if (pad) {
-                v0 = v1 = v2 = v3 = 0;
-                w0 = w1 = w2 = w3 = PADW;
-            }
+            v0 &= keep, v1 &= keep, v2 &= keep, v3 &= keep;
+            w0 = v0 | (PADW & ~keep), w1 = v1 | (PADW & ~keep), w2 = v2 | (PADW & ~keep), w3 = v3 | (PADW & ~keep);
         }
         const uint32_t tie = (1u + (lane & 1)) * kR1;  // bit b = t & 1 of both halves
         if (lane < kChunk) {
@@ -251,13 +268,14 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     load_raw(0, ra, rb);
     stage(0, ra, rb);
     load_raw(1, ra, rb);
-    // software pipeline: the table pairs of group G+2 are read while group G computes
-    uint2 cur[6], nx1[6];
+    // software pipeline: the table pairs of group G+3 are read while group G computes, into
+    // the slot of a four-group register ring (8 groups per chunk: no copies at the loop edge)
+    uint2 buf[4][6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-        cur[k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * k);
-        nx1[k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * (6 + k));
-    }
+    for (int g = 0; g < 3; g++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * (6 * g + k));
+    const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t acc = 0, dd = 0;
     const int tacs = (dbg & 2) ? 0 : Tpad;
@@ -266,7 +284,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
-        uint32_t* dchunk = dec + (t0 >> 4) * 64 + lane;
+        uint32_t* dchunk = dec + (t0 >> 4) * 64 + widx;
 
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
@@ -286,19 +304,15 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     }
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
-        uint2 nx2[6];                                                                             \
-        _Pragma("unroll") for (int k = 0; k < 6; k++) nx2[k] =                                    \
-            ap[k][(6 * ((G) + 2) + k) % kChunk];                              \
-        if ((G) == 5 && VTB_EXP_STAGE) {                                                          \
+        if ((G) == 5 && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */           \
             stage(c0 + 1, ra, rb);                                                                \
             load_raw(c0 + 2, ra, rb);                                                             \
         }                                                                                         \
+        _Pragma("unroll") for (int k = 0; k < 6; k++) buf[((G) + 3) & 3][k] =                     \
+            ap[k][(6 * ((G) + 3) + k) % kChunk];                                                  \
+        uint2* cur = buf[(G) & 3];                                                                \
         VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1) VTB_STEP(6 * (G) + 2, 2)                \
         VTB_STEP(6 * (G) + 3, 3) VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                \
-        _Pragma("unroll") for (int k = 0; k < 6; k++) {                                           \
-            cur[k] = nx1[k];                                                                      \
-            nx1[k] = nx2[k];                                                                      \
-        }                                                                                         \
     }
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
@@ -309,49 +323,63 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 
     // ---------------- traceback: verified block-parallel chains ----------------
     const int f = lane >> 5, blk = lane & 31;
-    const uint8_t* decf = reinterpret_cast<const uint8_t*>(dec) + 2 * f;  // this frame's 16-bit half
+    const uint32_t cb0 = uint32_t(r0 + 2 * f);  // this frame's 16-bit half of the word columns
     uint8_t* ob = tab + f * 4 * tbb;                                      // decoded bytes, index t/8
     const int top = (blk + 1) * tbb;
     const int start_full = top + kTbWarm;
     const int start = min(start_full, Tpad);
     const bool known = start >= T;  // walk starts on the known path (location 0 at and past T)
-    const int nbody = (kTbWarm + tbb) / 48;
-    uint32_t loc = 0, loc_top = 0;
+    const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;  // dbg bit 3: warm-up walk only
+    uint32_t loc = 0, loc_top = 0;  // survivor location as 4 l'
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {  // lane's walk has begun (start is a multiple of 48)
-            const uint64_t bits = tb_body(decf, tlo, loc);
+            const uint64_t bits = tb_body(cb0 + 256 * (tlo >> 4), loc);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
+    // Verification, all blocks at once: a block is right if it entered on its successor's
+    // exit location and that successor is proven, i.e. every later block of the frame checks
+    // (the last blocks are known).  Failed blocks whose successor is proven re-walk from it;
+    // a re-walk can change their exit, so the checks repeat until every block is proven --
+    // one round when all blocks merged within the warm-up.
     uint32_t fin = loc;  // survivor's location at step blk * tbb
-    bool ok = known;
-    for (int round = 0; round < 32; round++) {
-        if (!__any(!ok)) break;
-        const uint32_t sf = __shfl_down(fin, 1);
-        const int sok = __shfl_down(ok ? 1 : 0, 1);
-        const bool cand = !ok && sok;
-        if (cand && loc_top == sf) ok = true;  // entered the block on the proven path
-        if (cand && !ok) {
+    bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement only): skip verification
+    for (int round = 0; round < 33; round++) {
+        const uint32_t sf = __shfl_down(fin, 1);  // lane 31 (frame A's last block) is known
+        const bool ok = fixed || loc_top == sf;
+        const uint64_t bad = ~__ballot(ok);
+        if (bad == 0) break;
+        const uint32_t badf = uint32_t(bad >> (32 * f));       // this frame's failed blocks
+        const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+        if (!ok && succ_proven) {
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb_body(decf, tlo, loc));
+                put_bits48(ob, tlo, tb_body(cb0 + 256 * (tlo >> 4), loc));
             }
             fin = loc;
-            ok = true;
+            fixed = true;
         }
     }
     __syncthreads();
 
     // copy the decoded bytes out (bits past L are zero: the survivor ends in state 0)
     const int nbytes = (L + 7) >> 3;
-    uint8_t* oa = out + fa * out_stride;
-    for (int i = lane; i < nbytes; i += 64) oa[i] = tab[i];
-    if (has_b) {
-        uint8_t* o2 = out + fb * out_stride;
-        for (int i = lane; i < nbytes; i += 64) o2[i] = tab[4 * tbb + i];
+    const bool words = ((nbytes | out_stride | (size_t)out) & 3) == 0;  // wave-uniform
+    if (words) {  // lanes 0-31 copy frame A, 32-63 frame B, one dword each per pass
+        uint8_t* o = out + (f ? fb : fa) * out_stride;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(tab + f * 4 * tbb);
+        if (f == 0 || has_b)
+            for (int i = blk; i < (nbytes >> 2); i += 32) reinterpret_cast<uint32_t*>(o)[i] = src[i];
+    } else {
+        uint8_t* oa = out + fa * out_stride;
+        for (int i = lane; i < nbytes; i += 64) oa[i] = tab[i];
+        if (has_b) {
+            uint8_t* o2 = out + fb * out_stride;
+            for (int i = lane; i < nbytes; i += 64) o2[i] = tab[4 * tbb + i];
+        }
     }
 }
 

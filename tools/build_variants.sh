@@ -16,7 +16,8 @@ for v in "$@"; do
     nocmp) build nocmp -DVTB_EXP_NO_CMP ;;
     nostore_nolds) build nostore_nolds -DVTB_EXP_NO_STORE -DVTB_EXP_NO_LDS ;;
     nostage) build nostage -DVTB_EXP_NO_STAGE ;;
-    k15) build k15 -DVTB_EXP_K15 ;;
+    warm96) build warm96 -DVTB_EXP_TBWARM=96 ;;
+    warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;
