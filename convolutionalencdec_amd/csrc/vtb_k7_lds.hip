@@ -127,6 +127,8 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     }
 }
 
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (a & mask) | (b & ~mask); }
+
 // Reversed location numbering for the survivor words and the traceback: l' = rev6(l), so
 // step t's pairing bit is bit t mod 6 of l' and a window's two decisions (even step at
 // the lower history bit) land on the adjacent bits (t_even mod 6, t_odd mod 6) of l'.
@@ -147,7 +149,7 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4) {
     for (int j = 0; j < 24; j++) {
         const int todd = 47 - 2 * j;  // odd step of the window, relative to tlo
         if (j % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - j / 3));  // sextet end tlo + todd + 1
-        const int sh = 14 - 2 * ((todd & 15) >> 1);                           // window's bits in its half-word
+        const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);      // window's bits in its half-word
         uint32_t v;  // survivor half-word (smem is LDS address 0: dynamic LDS only)
         asm volatile("ds_read_u16 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"((todd >> 4) * 256));
         const int pos = 2 + (todd - 1) % 6;  // address bit of l' bit (t_even mod 6)
@@ -171,13 +173,21 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 // Measurement-only variants (tools/build_variants.sh builds them into separate libraries,
 // never the shipped one; their outputs are wrong): no table staging inside the ACS loop /
 // no survivor-word stores.
+#ifndef VTB_EXP_AHEAD
+#define VTB_EXP_AHEAD 2
+#endif
+#ifdef VTB_EXP_NO_TABREAD
+#define VTB_EXP_TABREAD(rd, reg) make_uint2((reg).y, (reg).x)
+#else
+#define VTB_EXP_TABREAD(rd, reg) (rd)
+#endif
 #ifdef VTB_EXP_NO_STAGE
 #define VTB_EXP_STAGE false
 #else
 #define VTB_EXP_STAGE true
 #endif
 #ifdef VTB_EXP_NO_WORD
-#define VTB_EXP_WORD(x) asm volatile("" ::"v"(acc))
+#define VTB_EXP_WORD(x) asm volatile("" ::"v"(z))
 #else
 #define VTB_EXP_WORD(x) x
 #endif
@@ -211,25 +221,29 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     }
 
     // Table staging: lane r < 48 builds the row of step 48c + r from the raw input bytes of
-    // that step (soft q0 | q1 << 8, hard the byte), loaded one chunk earlier and first
-    // touched (behind an empty asm, so the compiler cannot hoist the unpacking next to the
-    // load) when the chunk is staged.
+    // that step (soft q0 | q1 << 8, hard the byte).  The loads are issued in asm at the start
+    // of the chunk before (so no compiler-placed use -- e.g. a zero-extension -- can pull
+    // their wait up) and waited for where the chunk is staged, 36+ steps later.
+    const int srow = lane < kChunk ? lane : lane - kChunk;  // staging row (lanes 48-63 duplicate 0-15)
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
-        const int t = c * kChunk + (lane < kChunk ? lane : 0);
-        const int tc = t < T ? t : T - 1;
+        const int t = c * kChunk + srow;
+        const size_t tc = size_t(t < T ? t : T - 1);
         if constexpr (SOFT) {
-            unsigned short x, y;
-            __builtin_memcpy(&x, inA + 2 * (size_t)tc, 2);
-            __builtin_memcpy(&y, inB + 2 * (size_t)tc, 2);
-            ra = x;
-            rb = y;
+            asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off"
+                         : "=&v"(ra), "=&v"(rb) : "v"(inA + 2 * tc), "v"(inB + 2 * tc));
         } else {
-            ra = inA[tc];
-            rb = inB[tc];
+            asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
+                         : "=&v"(ra), "=&v"(rb) : "v"(inA + tc), "v"(inB + tc));
         }
     };
-    auto stage = [&](int c, uint32_t ra, uint32_t rb) {
-        asm volatile("" : "+v"(ra), "+v"(rb));
+    // Row values of the lane's step: e[c] = 4e(c) and et[c] = 4e(c) + tie (tie bit b = t & 1
+    // in both halves).  Branch-free, so the compiler can interleave it with ACS steps.
+    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4]) {
+#ifdef VTB_EXP_RAWNOWAIT
+        ra = lane * 0x0101u, rb = lane * 0x0303u;  // measurement only: no wait for the loads
+#else
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+#endif
         // packed [frame A, frame B] received values of coded bits 0 and 1, times four
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
         uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
@@ -241,43 +255,50 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         q1 <<= 2;
         // 4e of labels 0..3 (bit 0 of a label <-> coded bit 0); halves never borrow
         constexpr uint32_t QQ = 4 * Q * kR1;
-        const uint32_t e0 = q0 + q1, e1 = (QQ + q1) - q0, e2 = 2 * QQ - e1, e3 = 2 * QQ - e0;
-        uint32_t v0 = e0, v1 = e1, v2 = e2, v3 = e3, w0 = e0, w1 = e1, w2 = e2, w3 = e3;
-        if ((c + 1) * kChunk > T) {  // chunk reaches past T: padding rows (wave-uniform branch)
-            const uint32_t keep = c * kChunk + lane < T ? ~0u : 0u;
+        e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
+        const uint32_t tie = (1u + (srow & 1)) * kR1;
+#pragma unroll
+        for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
+    };
+    // Column k = c + 4R of the ring holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
+    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
+        uint2* col = reinterpret_cast<uint2*>(tab) + srow;  // column k at col[kCol * k]
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            col[k * kCol] = make_uint2(e[k], et[3 - k]);
+            col[(4 + k) * kCol] = make_uint2(et[k], e[3 - k]);
+        }
+        if ((c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows (last chunk only)
             constexpr uint32_t PADW = 4 * (12 * Q + 1) * kR1;
-            v0 &= keep, v1 &= keep, v2 &= keep, v3 &= keep;
-            w0 = v0 | (PADW & ~keep), w1 = v1 | (PADW & ~keep), w2 = v2 | (PADW & ~keep), w3 = v3 | (PADW & ~keep);
+            const uint32_t tie = et[0] - e[0];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                col[k * kCol] = make_uint2(0u, PADW + tie);
+                col[(4 + k) * kCol] = make_uint2(tie, PADW);
+            }
         }
-        const uint32_t tie = (1u + (lane & 1)) * kR1;  // bit b = t & 1 of both halves
-        if (lane < kChunk) {
-            uint2* col = reinterpret_cast<uint2*>(tab) + lane;  // column k at col[kCol * k]
-            col[0 * kCol] = make_uint2(v0, w3 + tie);  // (c, R = 0)
-            col[1 * kCol] = make_uint2(v1, w2 + tie);
-            col[2 * kCol] = make_uint2(v2, w1 + tie);
-            col[3 * kCol] = make_uint2(v3, w0 + tie);
-            col[4 * kCol] = make_uint2(v0 + tie, w3);  // (c, R = 1)
-            col[5 * kCol] = make_uint2(v1 + tie, w2);
-            col[6 * kCol] = make_uint2(v2 + tie, w1);
-            col[7 * kCol] = make_uint2(v3 + tie, w0);
-        }
+    };
+    auto stage = [&](int c, uint32_t ra, uint32_t rb) {
+        uint32_t e[4], et[4];
+        stage_compute(ra, rb, e, et);
+        stage_write(c, e, et);
     };
 
     uint32_t M = (lane == 0) ? kBias4 * kR1 : (kBias4 + 4 * INIT) * kR1;
     uint32_t ra, rb;
     load_raw(0, ra, rb);
     stage(0, ra, rb);
-    load_raw(1, ra, rb);
     // software pipeline: the table pairs of group G+3 are read while group G computes, into
     // the slot of a four-group register ring (8 groups per chunk: no copies at the loop edge)
     uint2 buf[4][6];
+    constexpr int AH = VTB_EXP_AHEAD;  // groups read ahead (2 or 3)
 #pragma unroll
-    for (int g = 0; g < 3; g++)
+    for (int g = 0; g < AH; g++)
 #pragma unroll
         for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * (6 * g + k));
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
-    uint32_t acc = 0, dd = 0;
+    uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
     const int tacs = (dbg & 2) ? 0 : Tpad;
     for (int t0 = 0; t0 < tacs; t0 += kChunk) {
         const int c0 = t0 / kChunk;
@@ -290,26 +311,36 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     {                                                                                            \
         if (((I) % 12) == 10) {                                                                  \
             /* renormalisation reference: location 0 (lane 0), history clear at this point */    \
-            dd = kBias4 * kR1 - __builtin_amdgcn_readfirstlane(M);                                \
+            const uint32_t ref = __builtin_amdgcn_readfirstlane(M);                              \
+            asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(kBias4 * kR1), "s"(ref) : "scc");        \
         }                                                                                        \
         uint32_t A, B;                                                                           \
         candidates<5 - (PH)>(M, cur[PH], A, B);                                                  \
         M = pk_min(A, B);                                                                        \
         if ((I) & 1) {                                                                           \
-            const uint32_t x = M & kHist;                                                        \
-            M = (((I) % 12) == 11) ? ((M ^ x) + dd) : (M ^ x);                                   \
-            acc = (((I) & 15) == 1) ? x : ((acc << 2) | x);                                      \
-            if (((I) & 15) == 15) VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = acc);                   \
+            /* window (I) >> 1 & 7 of the word: history bytes of two windows by one v_perm */    \
+            const int w = ((I) & 15) >> 1;                                                       \
+            if (w & 1) pw[w >> 1] = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
+            else m_prev = M;                                                                     \
+            M = (((I) % 12) == 11) ? ((M & ~kHist) + dd) : (M & ~kHist);                         \
+            if (((I) & 15) == 15) {                                                              \
+                /* bits 2j..2j+1 of byte (w & 1): window w = 2j + (w & 1) */                     \
+                uint32_t z = bfi(0x03030303u, pw[0], pw[1] << 2);                                \
+                z = bfi(0x0F0F0F0Fu, z, pw[2] << 4);                                             \
+                z = bfi(0x3F3F3F3Fu, z, pw[3] << 6);                                             \
+                VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = z);                                       \
+            }                                                                                    \
         }                                                                                        \
     }
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
-        if ((G) == 5 && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */           \
-            stage(c0 + 1, ra, rb);                                                                \
-            load_raw(c0 + 2, ra, rb);                                                             \
+        if ((G) == 0) load_raw(c0 + 1, ra, rb);                                                   \
+        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set);                            \
+        if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
+            stage_write(c0 + 1, se, set);                                                         \
         }                                                                                         \
-        _Pragma("unroll") for (int k = 0; k < 6; k++) buf[((G) + 3) & 3][k] =                     \
-            ap[k][(6 * ((G) + 3) + k) % kChunk];                                                  \
+        _Pragma("unroll") for (int k = 0; k < 6; k++) buf[((G) + AH) & 3][k] =                    \
+            VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + k) % kChunk], buf[(G) & 3][k]);                \
         uint2* cur = buf[(G) & 3];                                                                \
         VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1) VTB_STEP(6 * (G) + 2, 2)                \
         VTB_STEP(6 * (G) + 3, 3) VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                \

@@ -16,6 +16,10 @@ for v in "$@"; do
     nocmp) build nocmp -DVTB_EXP_NO_CMP ;;
     nostore_nolds) build nostore_nolds -DVTB_EXP_NO_STORE -DVTB_EXP_NO_LDS ;;
     nostage) build nostage -DVTB_EXP_NO_STAGE ;;
+    ahead3) build ahead3 -DVTB_EXP_AHEAD=3 ;;
+    notabread) build notabread -DVTB_EXP_NO_TABREAD ;;
+    notab) build notab -DVTB_EXP_NO_TABREAD -DVTB_EXP_NO_STAGE ;;
+    rawnowait) build rawnowait -DVTB_EXP_RAWNOWAIT ;;
     warm96) build warm96 -DVTB_EXP_TBWARM=96 ;;
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
