@@ -339,10 +339,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
             stage_write(c0 + 1, se, set);                                                         \
         }                                                                                         \
+        uint2* cur = buf[(G) & 3];                                                                \
+        VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1)                                         \
         _Pragma("unroll") for (int k = 0; k < 6; k++) buf[((G) + AH) & 3][k] =                    \
             VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + k) % kChunk], buf[(G) & 3][k]);                \
-        uint2* cur = buf[(G) & 3];                                                                \
-        VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1) VTB_STEP(6 * (G) + 2, 2)                \
+        VTB_STEP(6 * (G) + 2, 2)                                                                  \
         VTB_STEP(6 * (G) + 3, 3) VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                \
     }
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
