@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--gen", choices=("host", "device"), default="host",
+                    help="synthetic frames from numpy on the host (default) or from the device generator "
+                         "(csrc/vtb_gen.hip: no PCIe, for large batches)")
     return ap.parse_args()
 
 
@@ -171,9 +174,19 @@ def main():
     soft = not args.hard
     F, L = args.frames, args.frame_bits
     T = L + code[0] - 1
-    unc, rx = synth.make_frames(code[0], code[1], F, L, soft=soft, snr_db=args.snr_db, p=0.0559, seed=shard_seed(rank))
+    if args.gen == "device":
+        from convolutionalencdec_amd import frames as devframes
+
+        d_unc, d_rx = devframes.make_frames(ConvCode(*code), F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
+                                            seed=shard_seed(rank), device=local)
+        x = d_rx.reshape(F, -1)
+        torch.cuda.synchronize(dev)
+        unc = d_unc.cpu().numpy()
+    else:
+        unc, rx = synth.make_frames(code[0], code[1], F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
+                                    seed=shard_seed(rank))
+        x = torch.from_numpy(rx.reshape(F, -1)).to(dev)
     dec = ViterbiDecoder(ConvCode(*code), frame_bits=L, soft=soft, device=local)
-    x = torch.from_numpy(rx.reshape(F, -1)).to(dev)
     out = torch.empty((F, (L + 7) // 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -226,7 +239,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u16",
-        "data": "synthetic",
+        "data": "synthetic" if args.gen == "host" else "synthetic (device generator)",
         "config": {
             "workload": f"K={code[0]} r=1/2 {'8-bit soft' if soft else 'hard'}-decision Viterbi, {F} frames x {L} "
                         f"info bits per GPU, AWGN SNR {args.snr_db:g} dB" if soft else

@@ -37,6 +37,12 @@ EXPORTED_SYMBOLS = (
     "vtb_decode_host_multi",
     "vtb_decode_frame_legacy",
     "vtb_device_count",
+    "vtb_rand64",
+    "vtb_payload_device",
+    "vtb_encode_device",
+    "vtb_channel_device",
+    "vtb_awgn_kq",
+    "vtb_bsc_p32",
 )
 
 
@@ -93,8 +99,19 @@ def lib():
     L.vtb_decode_host_multi.argtypes = [cp, ctypes.c_int, i32, vp, vp, sz, ctypes.c_uint32]
     L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
     L.vtb_device_count.argtypes = []
+    u64 = ctypes.c_uint64
+    L.vtb_rand64.restype = u64
+    L.vtb_rand64.argtypes = [u64, u64, u64]
+    L.vtb_payload_device.argtypes = [u64, i32, vp, sz, sz, vp]
+    L.vtb_encode_device.argtypes = [cp, i32, vp, sz, vp, sz, sz, vp]
+    L.vtb_channel_device.argtypes = [ctypes.c_int, ctypes.c_double, u64, vp, sz, i32, vp, sz, sz, vp]
+    L.vtb_awgn_kq.restype = ctypes.c_int64
+    L.vtb_awgn_kq.argtypes = [ctypes.c_double]
+    L.vtb_bsc_p32.restype = ctypes.c_uint32
+    L.vtb_bsc_p32.argtypes = [ctypes.c_double]
     for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
-                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_device_count"):
+                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_device_count", "vtb_payload_device",
+                 "vtb_encode_device", "vtb_channel_device"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -16,6 +16,11 @@
  *                            layout; soft input is the build-defined 8-bit extension)
  *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
  *                           behind include/viterbiDecoder.h (VITERBI_DECODER_HARD)
+ *   vtb_encode_device       convEnc                       src/convEncode.c:46-130
+ *                           (whole terminated frames, batched on the device)
+ *   vtb_payload_device /    the harnesses' random payloads and BSC corruption
+ *   vtb_channel_device      (berTestK7.c:22-43, 135-138; speedDecode.c:38-60), re-specified
+ *                           with a counter-based RNG so the device generates bulk frames
  *
  * Data layout (frame-major, reference layout per frame):
  *   hard input   T = L + K - 1 bytes per frame, byte t = coded segment t, bit i = output of
@@ -115,6 +120,43 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
 
 /* Number of gfx950 devices visible (0 if none); negative VTB_ERR_DEVICE on runtime error. */
 int vtb_device_count(void);
+
+/* ---- Synthetic frames on the device -------------------------------
+ * Randomness is one counter-based stream, integer-exact on any host or device:
+ *   mix64(x)                 = splitmix64 finalizer (x ^= x>>30; x *= 0xBF58476D1CE4E5B9;
+ *                              x ^= x>>27; x *= 0x94D049BB133111EB; x ^= x>>31)
+ *   vtb_rand64(seed, f, c)   = mix64(mix64(seed + 0x9E3779B97F4A7C15*(f+1)) ^ 0xD1B54A32D192ED03*(c+1))
+ * Kernels run on the calling thread's current HIP device, asynchronously on `stream`. */
+uint64_t vtb_rand64(uint64_t seed, uint64_t frame, uint64_t ctr);
+
+/* Payload: byte j of frame f = byte (j mod 8) of vtb_rand64(seed, f, j / 8) (little-endian);
+ * bits past frame_bits in the last byte are cleared (MSB-first packing). */
+int vtb_payload_device(uint64_t seed, int32_t frame_bits, uint8_t* d_out, size_t stride, size_t frames,
+                       void* stream);
+
+/* convEnc (src/convEncode.c:46-130) on whole terminated frames: rows of ceil(L/8) payload
+ * bytes (MSB-first) -> rows of L + K - 1 coded segment bytes (bit i = generator i), the last
+ * K - 1 of them the zero tail.  Payload bits past L are ignored. */
+int vtb_encode_device(const vtb_code_t* code, int32_t frame_bits, const uint8_t* d_uncoded, size_t in_stride,
+                      uint8_t* d_coded, size_t out_stride, size_t frames, void* stream);
+
+/* Channel over rows of `segments` hard coded segments:
+ *   VTB_INPUT_HARD   BSC, param = crossover p: coded bit i of segment t flips iff 32-bit
+ *                    half i of vtb_rand64(seed, f, t) < vtb_bsc_p32(p); output hard bytes.
+ *   VTB_INPUT_SOFT8  BPSK (0 -> +1) + AWGN at param = SNR dB (sigma = sqrt(1/(2 Es/N0)),
+ *                    Es/N0 = SNR + 10 log10 4, as berTestK7's SNR column) + the 8-bit soft
+ *                    quantiser q = round((1 - y) * 127.5) clamped to [0, 255], in fixed
+ *                    point: z_fx = sum of twelve 21-bit fields (bits 0-20, 21-41, 42-62 of
+ *                    vtb_rand64(seed, f, 8t + 4i + h), h = 0..3) - 6*2^21;
+ *                    q = clamp(floor((b*255*2^16 - floor(vtb_awgn_kq(snr) * z_fx / 2^21)
+ *                    + 2^15) / 2^16), 0, 255); output 2 bytes per segment. */
+int vtb_channel_device(vtb_input_t output, double param, uint64_t seed, const uint8_t* d_coded, size_t in_stride,
+                       int32_t segments, uint8_t* d_rx, size_t out_stride, size_t frames, void* stream);
+
+/* Fixed-point channel constants used above: round(sigma(snr) * 127.5 * 2^16) and
+ * floor(p * 2^32) (saturating). */
+int64_t vtb_awgn_kq(double snr_db);
+uint32_t vtb_bsc_p32(double p);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
  */
 #include "viterbi_oracle.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -319,4 +320,92 @@ long oracle_bit_errors(const uint8_t* a, const uint8_t* b, size_t len) {
     long e = 0;
     for (size_t i = 0; i < len; i++) e += __builtin_popcount((unsigned)(a[i] ^ b[i]));
     return e;
+}
+
+/* ---- device frame generator checker (specification: include/viterbi_amd.h) ---- */
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+uint64_t oracle_rand64(uint64_t seed, uint64_t frame, uint64_t ctr) {
+    return mix64(mix64(seed + 0x9E3779B97F4A7C15ull * (frame + 1)) ^ (0xD1B54A32D192ED03ull * (ctr + 1)));
+}
+
+void oracle_gen_payload(uint64_t seed, int bits, uint8_t* out, size_t stride, size_t frames) {
+    const int nbytes = (bits + 7) / 8;
+    for (size_t f = 0; f < frames; f++)
+        for (int j = 0; j < nbytes; j++) {
+            unsigned v = (unsigned)(oracle_rand64(seed, f, (uint64_t)(j / 8)) >> (8 * (j % 8))) & 0xFFu;
+            if (j == nbytes - 1 && (bits % 8)) v &= (0xFFu << (8 - bits % 8)) & 0xFFu;
+            out[f * stride + j] = (uint8_t)v;
+        }
+}
+
+/* Bit-serial restatement of convEnc: shift each information bit (MSB-first) into the
+ * tapped delay line's LSB and emit parity(delay & reverse_K(g_j)) as bit j
+ * (convEncode.c:63-97, 132-161); then K-1 zero shifts (:100-122). */
+void oracle_gen_encode(int K, const uint64_t g[2], int bits, const uint8_t* unc, size_t in_stride, uint8_t* coded,
+                       size_t out_stride, size_t frames) {
+    uint64_t rg[2] = {0, 0};
+    for (int j = 0; j < 2; j++)
+        for (int i = 0; i < K; i++) rg[j] |= ((g[j] >> i) & 1u) << (K - 1 - i);
+    const uint64_t mask = (1ull << K) - 1;
+    for (size_t f = 0; f < frames; f++) {
+        uint64_t delay = 0;
+        for (int t = 0; t < bits + K - 1; t++) {
+            const unsigned b = t < bits ? (unc[f * in_stride + t / 8] >> (7 - t % 8)) & 1u : 0u;
+            delay = ((delay << 1) | b) & mask;
+            coded[f * out_stride + t] =
+                (uint8_t)((__builtin_popcountll(delay & rg[0]) & 1) | ((__builtin_popcountll(delay & rg[1]) & 1) << 1));
+        }
+    }
+}
+
+void oracle_gen_bsc(uint64_t seed, uint32_t p32, int T, const uint8_t* coded, size_t in_stride, uint8_t* rx,
+                    size_t out_stride, size_t frames) {
+    for (size_t f = 0; f < frames; f++)
+        for (int t = 0; t < T; t++) {
+            const uint64_t r = oracle_rand64(seed, f, (uint64_t)t);
+            unsigned c = coded[f * in_stride + t] & 3u;
+            if ((uint32_t)r < p32) c ^= 1u;
+            if ((uint32_t)(r >> 32) < p32) c ^= 2u;
+            rx[f * out_stride + t] = (uint8_t)c;
+        }
+}
+
+void oracle_gen_awgn8(uint64_t seed, int64_t kq, int T, const uint8_t* coded, size_t in_stride, uint8_t* rx,
+                      size_t out_stride, size_t frames) {
+    for (size_t f = 0; f < frames; f++)
+        for (int t = 0; t < T; t++)
+            for (int i = 0; i < 2; i++) {
+                int64_t z = -(6ll << 21);
+                for (int h = 0; h < 4; h++) {
+                    const uint64_t r = oracle_rand64(seed, f, 8ull * (uint64_t)t + 4u * (unsigned)i + (unsigned)h);
+                    z += (int64_t)(r & 0x1FFFFF) + (int64_t)((r >> 21) & 0x1FFFFF) + (int64_t)((r >> 42) & 0x1FFFFF);
+                }
+                const int64_t prod = kq * z;
+                const int64_t v = prod >= 0 ? prod / (1 << 21) : -((-prod + (1 << 21) - 1) / (1 << 21)); /* floor */
+                const int b = (coded[f * in_stride + t] >> i) & 1;
+                const int64_t qf = (b ? (255ll << 16) : 0) - v + 32768;
+                int64_t q = qf >= 0 ? qf / 65536 : -((-qf + 65535) / 65536); /* floor */
+                q = q < 0 ? 0 : (q > 255 ? 255 : q);
+                rx[f * out_stride + 2 * (size_t)t + i] = (uint8_t)q;
+            }
+}
+
+int64_t oracle_awgn_kq(double snr_db) {
+    const double esn0 = pow(10.0, (snr_db + 10.0 * log10(4.0)) / 10.0);
+    return (int64_t)llround(sqrt(1.0 / (2.0 * esn0)) * 127.5 * 65536.0);
+}
+
+uint32_t oracle_bsc_p32(double p) {
+    if (!(p > 0.0)) return 0u;
+    if (p >= 1.0) return 0xFFFFFFFFu;
+    return (uint32_t)floor(p * 4294967296.0);
 }

@@ -42,7 +42,49 @@ class Oracle:
         L.oracle_stream_decode.argtypes = [v, v, i, v, i, v]
         L.oracle_bertest_stream.restype = ctypes.c_long
         L.oracle_bertest_stream.argtypes = [i, v, ctypes.c_uint, i, v, i, i, v, v]
+        u64 = ctypes.c_uint64
+        L.oracle_rand64.restype = u64
+        L.oracle_rand64.argtypes = [u64, u64, u64]
+        L.oracle_gen_payload.argtypes = [u64, i, v, sz, sz]
+        L.oracle_gen_encode.argtypes = [i, v, i, v, sz, v, sz, sz]
+        L.oracle_gen_bsc.argtypes = [u64, ctypes.c_uint32, i, v, sz, v, sz, sz]
+        L.oracle_gen_awgn8.argtypes = [u64, ctypes.c_int64, i, v, sz, v, sz, sz]
+        L.oracle_awgn_kq.restype = ctypes.c_int64
+        L.oracle_awgn_kq.argtypes = [ctypes.c_double]
+        L.oracle_bsc_p32.restype = ctypes.c_uint32
+        L.oracle_bsc_p32.argtypes = [ctypes.c_double]
         self.L = L
+
+    # -- device frame generator checker (include/viterbi_amd.h "Synthetic frames") --
+    def rand64(self, seed, frame, ctr):
+        return int(self.L.oracle_rand64(seed, frame, ctr))
+
+    def gen_payload(self, seed, bits, frames):
+        nb = (bits + 7) // 8
+        out = np.zeros((frames, nb), np.uint8)
+        self.L.oracle_gen_payload(seed, bits, vp(out), nb, frames)
+        return out
+
+    def gen_encode(self, K, g, bits, unc):
+        unc = np.ascontiguousarray(unc, np.uint8)
+        T = bits + K - 1
+        out = np.zeros((unc.shape[0], T), np.uint8)
+        self.L.oracle_gen_encode(K, self._g(g), bits, vp(unc), unc.shape[1], vp(out), T, unc.shape[0])
+        return out
+
+    def gen_bsc(self, seed, p32, coded):
+        coded = np.ascontiguousarray(coded, np.uint8)
+        F, T = coded.shape
+        out = np.zeros((F, T), np.uint8)
+        self.L.oracle_gen_bsc(seed, p32, T, vp(coded), T, vp(out), T, F)
+        return out
+
+    def gen_awgn8(self, seed, kq, coded):
+        coded = np.ascontiguousarray(coded, np.uint8)
+        F, T = coded.shape
+        out = np.zeros((F, T, 2), np.uint8)
+        self.L.oracle_gen_awgn8(seed, kq, T, vp(coded), T, vp(out), 2 * T, F)
+        return out
 
     @staticmethod
     def _g(g):

@@ -1,0 +1,81 @@
+"""GPU: the device frame generator (csrc/vtb_gen.hip) byte for byte against the oracle's
+restatement, the device encoder against the reference's golden frames, and an end-to-end
+device-generated batch decoded on the GPU against the oracle decoder."""
+import numpy as np
+import pytest
+
+from helpers import CODES, Oracle, golden_sets
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, ViterbiDecoder, frames, native  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+@pytest.mark.parametrize("L", [1, 13, 1021, 1024, 2048])
+def test_payload(orc, L):
+    d = frames.payload(37, L, seed=9865)
+    torch.cuda.synchronize()
+    assert (d.cpu().numpy() == orc.gen_payload(9865, L, 37)).all()
+
+
+@pytest.mark.parametrize("K", [5, 7, 9])
+def test_encode_golden(K):
+    """Device encoder on the reference's own error-free golden frames."""
+    for key, L, unc, rx, _ in golden_sets(K):
+        if not key.endswith("p000"):
+            continue
+        out = frames.encode(ConvCode(K, CODES[K]), L, torch.from_numpy(unc).cuda())
+        assert (out.cpu().numpy() == rx).all(), key
+
+
+@pytest.mark.parametrize("K,L", [(3, 7), (7, 1), (7, 13), (7, 1024), (9, 1021)])
+def test_encode_random(orc, K, L):
+    g = CODES.get(K, (0o7, 0o5))
+    unc = orc.gen_payload(5, L, 64)
+    unc_dirty = unc.copy()
+    if L % 8:
+        unc_dirty[:, -1] |= np.uint8(0xFF >> (L % 8))  # pad bits must be ignored
+    out = frames.encode(ConvCode(K, g), L, torch.from_numpy(unc_dirty).cuda())
+    assert (out.cpu().numpy() == orc.gen_encode(K, g, L, unc)).all()
+
+
+@pytest.mark.parametrize("p", [0.0, 0.0559, 0.5])
+def test_bsc(orc, p):
+    coded = torch.from_numpy(orc.gen_payload(3, 8 * 1030, 50)).cuda()  # arbitrary segment bytes
+    rx = frames.channel(coded, soft=False, param=p, seed=77)
+    assert (rx.cpu().numpy() == orc.gen_bsc(77, frames.bsc_p32(p), coded.cpu().numpy() & 3)).all()
+
+
+@pytest.mark.parametrize("snr", [-5.0, -3.0, 3.0])
+def test_awgn(orc, snr):
+    coded = torch.from_numpy(orc.gen_payload(4, 8 * 1030, 50) & 3).cuda()
+    rx = frames.channel(coded, soft=True, param=snr, seed=123)
+    assert (rx.cpu().numpy() == orc.gen_awgn8(123, frames.awgn_kq(snr), coded.cpu().numpy())).all()
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_end_to_end(orc, soft):
+    """Device-generated frames, decoded on the GPU, against the oracle decoder on the same
+    bytes; at a clean channel the payload comes back."""
+    K, L, F = 7, 1024, 256
+    code = ConvCode(K, CODES[K])
+    unc, rx = frames.make_frames(code, F, L, soft=soft, snr_db=-4.0, p=0.03, seed=21)
+    dec = ViterbiDecoder(code, frame_bits=L, soft=soft)
+    out = dec.decode_device(rx.reshape(F, -1)).cpu().numpy()
+    ref = orc.decode(K, CODES[K], rx.cpu().numpy(), L, soft=soft)
+    assert (out == ref).all()
+    unc2, rx2 = frames.make_frames(code, F, L, soft=soft, snr_db=10.0, p=0.0, seed=22)
+    assert (dec.decode_device(rx2.reshape(F, -1)).cpu().numpy() == unc2.cpu().numpy()).all()
