@@ -127,7 +127,12 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     }
 }
 
-__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) { return (a & mask) | (b & ~mask); }
+// One v_bfi_b32 (the compiler otherwise splits a constant-mask select into and/and/or).
+__device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+    return r;
+}
 
 // Reversed location numbering for the survivor words and the traceback: l' = rev6(l), so
 // step t's pairing bit is bit t mod 6 of l' and a window's two decisions (even step at
@@ -225,15 +230,17 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     // of the chunk before (so no compiler-placed use -- e.g. a zero-extension -- can pull
     // their wait up) and waited for where the chunk is staged, 36+ steps later.
     const int srow = lane < kChunk ? lane : lane - kChunk;  // staging row (lanes 48-63 duplicate 0-15)
+    // (wave-uniform frame bases in SGPRs, one 32-bit lane offset)
+    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA)), baseB = uniform64(reinterpret_cast<uint64_t>(inB));
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         const int t = c * kChunk + srow;
-        const size_t tc = size_t(t < T ? t : T - 1);
+        const uint32_t tc = uint32_t(t < T ? t : T - 1);
         if constexpr (SOFT) {
-            asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off"
-                         : "=&v"(ra), "=&v"(rb) : "v"(inA + 2 * tc), "v"(inB + 2 * tc));
+            asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
+                         : "=&v"(ra), "=&v"(rb) : "v"(2 * tc), "s"(baseA), "s"(baseB));
         } else {
-            asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
-                         : "=&v"(ra), "=&v"(rb) : "v"(inA + tc), "v"(inB + tc));
+            asm volatile("global_load_ubyte %0, %2, %3\n\tglobal_load_ubyte %1, %2, %4"
+                         : "=&v"(ra), "=&v"(rb) : "v"(tc), "s"(baseA), "s"(baseB));
         }
     };
     // Row values of the lane's step: e[c] = 4e(c) and et[c] = 4e(c) + tie (tie bit b = t & 1
@@ -325,9 +332,9 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             M = (((I) % 12) == 11) ? ((M & ~kHist) + dd) : (M & ~kHist);                         \
             if (((I) & 15) == 15) {                                                              \
                 /* bits 2j..2j+1 of byte (w & 1): window w = 2j + (w & 1) */                     \
-                uint32_t z = bfi(0x03030303u, pw[0], pw[1] << 2);                                \
-                z = bfi(0x0F0F0F0Fu, z, pw[2] << 4);                                             \
-                z = bfi(0x3F3F3F3Fu, z, pw[3] << 6);                                             \
+                uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
+                z = bfi_op(0x0F0F0F0Fu, z, pw[2] << 4);                                          \
+                z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
                 VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = z);                                       \
             }                                                                                    \
         }                                                                                        \
@@ -340,15 +347,18 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             stage_write(c0 + 1, se, set);                                                         \
         }                                                                                         \
         uint2* cur = buf[(G) & 3];                                                                \
+        /* table reads AH groups ahead, issued after the two permlane steps */                     \
         VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1)                                         \
-        _Pragma("unroll") for (int k = 0; k < 6; k++) buf[((G) + AH) & 3][k] =                    \
-            VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + k) % kChunk], buf[(G) & 3][k]);                \
-        VTB_STEP(6 * (G) + 2, 2)                                                                  \
-        VTB_STEP(6 * (G) + 3, 3) VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                \
+        VTB_RD(G, 0) VTB_RD(G, 1) VTB_RD(G, 2) VTB_RD(G, 3) VTB_RD(G, 4) VTB_RD(G, 5)             \
+        VTB_STEP(6 * (G) + 2, 2) VTB_STEP(6 * (G) + 3, 3)                                         \
+        VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                                         \
     }
+#define VTB_RD(G, k)                                                                              \
+    buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk], buf[(G) & 3][k]);
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
+#undef VTB_RD
     }
     __syncthreads();
     if (dbg & 1) return;
