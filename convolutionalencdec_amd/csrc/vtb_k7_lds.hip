@@ -50,24 +50,26 @@
 // kernel uses 12Q + 1.
 //
 // Renormalisation every 12 steps (subtract location 0's metric taken at the start of the
-// window, add a bias) folds into the history clear as one v_xad_u32; it replaces the
-// reference's uint8 renorm (exact metrics have a bounded spread).
+// window, add a bias) rides on the history clear; it replaces the reference's uint8 renorm
+// (exact metrics have a bounded spread).
 //
-// Survivors.  Each lane appends its two history bits per window to one VGPR (frame A in
-// bits 0..15, frame B in bits 16..31, oldest window highest) and every 16 steps the wave
-// writes its 64 words (256 B, one ds_write_b32) to LDS.
+// Survivors.  Two windows' history bytes are gathered by one v_perm, and every 16 steps
+// three v_bfi pack the 8 windows into one word per lane (frame A in bits 0..15, frame B in
+// 16..31; window w at bits 8(w & 1) + 2(w >> 1)), which the wave writes (256 B, one
+// ds_write_b32) to the slot of the lane's bit-reversed location l' = rev6(l).
 //
-// Traceback (reference :200-256), in location space, two steps per LDS read: from the
-// location at the end of a window, the word's two bits are the new location bits p_odd
-// and then p_even.  A sextet's six decoded bits are the location at its end (MSB = the
-// oldest step).  Lanes 0-31 trace blocks of frame A, lanes 32-63 of frame B, each block
-// of TBB steps (a multiple of 48) walking back from 48 steps past its end as a chain of
-// dependent LDS reads.  A block whose walk starts at or beyond T starts at the known
-// location 0 (the terminated path ends in state 0).  Every other block starts at a guess
-// and is verified: its location on entering the block must equal the location its
-// successor ended on; a block that disagrees is re-walked from its successor's proven
-// location.  So the output is exactly the reference's for every input; only the time
-// depends on how fast survivor paths merge.
+// Traceback (reference :200-256), two steps per LDS read: in l' numbering step t's
+// pairing bit is bit t mod 6, so a window's two decisions are the new bits
+// (t_even mod 6, t_odd mod 6) of l', adjacent; the walk keeps the LDS address of the
+// survivor's word and a window is one read, one shift and one bit-field insert.  A
+// sextet's six decoded bits are its end location (oldest step at bit 0 of l').  Lanes
+// 0-31 trace blocks of frame A, lanes 32-63 of frame B, each block of TBB steps (a
+// multiple of 48) walking back from 48 steps past its end.  A block whose walk starts at
+// or beyond T starts at the known location 0 (the terminated path ends in state 0).  The
+// others are verified together: a block is right if it entered on its successor's exit
+// location and its successor is proven; failed blocks re-walk from a proven successor
+// until all are proven.  So the output is exactly the reference's for every input; only
+// the time depends on how fast survivor paths merge.
 
 #include "vtb_k7_common.h"
 
