@@ -270,13 +270,18 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
     };
     // Column k = c + 4R of the ring holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
+    // (V, W) of a slot from two unrelated VGPRs by ds_write2_b32 (a ds_write_b64 would need
+    // them in a register pair: 8 moves per chunk); three bases keep offsets below 256 dwords.
+    const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
     auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
         uint2* col = reinterpret_cast<uint2*>(tab) + srow;  // column k at col[kCol * k]
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            col[k * kCol] = make_uint2(e[k], et[3 - k]);
-            col[(4 + k) * kCol] = make_uint2(et[k], e[3 - k]);
-        }
+#define VTB_W2(base, k, v, w)                                                                         \
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
+                 "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
+        VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
+        VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
+        VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+#undef VTB_W2
         if ((c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows (last chunk only)
             constexpr uint32_t PADW = 4 * (12 * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
