@@ -2,7 +2,8 @@
 // host/device entry points and the multi-GPU shard driver.
 //
 // Host-side only; the trellis work happens in the kernels of vtb_k7_lds.hip (K=7, the fast
-// path), vtb_reg_path.hip (K=7, long frames) and vtb_lds_path.hip (every K).
+// path, survivors in LDS or, for long frames, in a global workspace) and vtb_lds_path.hip
+// (every K).
 
 #include <hip/hip_runtime.h>
 
@@ -34,6 +35,7 @@ struct vtb_plan {
     // kernel workspace (survivor words), stream-ordered pool memory, grown on demand
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    int cus = 256;  // compute units of the device (kernel choice)
 };
 
 namespace {
@@ -105,12 +107,23 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
     const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
     hipError_t e;
-    // LDS-resident K=7 kernel while it keeps at least 4 waves per CU (2 frames per wave),
-    // else the global-workspace K=7 kernel, else the generic LDS-path kernel (every K).
-    if (want_k7 && vtb::k7_lds_supported(a) && (!any || vtb::k7_lds_bytes(a) <= 40 * 1024)) {
+    // K=7: survivors in LDS while that LDS leaves the CU as many waves (2 frames each) as
+    // the batch can give it, up to 2 per SIMD (the ACS is VALU-bound there: more waves do
+    // not help); else survivors in a global workspace (3 KB LDS per wave, traceback from
+    // L2/HBM).  Measured: 4096 x 1024 soft, LDS 36.4 us vs global 46.3 us;
+    // 65536 x 2048, LDS (1 wave per SIMD) 1.56 ms vs global 0.94 ms.  Other K: the generic
+    // LDS-path kernel.
+    bool k7_in_lds = false;
+    if (want_k7 && vtb::k7_lds_supported(a)) {
+        const size_t waves_per_cu = ((frames + 1) / 2 + p->cus - 1) / p->cus;
+        const size_t want = waves_per_cu < 8 ? waves_per_cu : 8;
+        const size_t fit = (160 * 1024) / vtb::k7_lds_bytes(a);
+        k7_in_lds = !any || fit >= want || !vtb::k7_global_supported(a);
+    }
+    if (k7_in_lds) {
         e = vtb::launch_k7_lds(a);
-    } else if (want_gws && vtb::reg_path_supported(a)) {
-        const size_t need = vtb::reg_path_workspace_bytes(a);
+    } else if (want_gws && vtb::k7_global_supported(a)) {
+        const size_t need = vtb::k7_global_workspace_bytes(a);
         if (need > p->ws_bytes) {
             if (p->ws) (void)vtb::workspace_free(p->ws, stream);
             p->ws = nullptr;
@@ -122,7 +135,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
             p->ws_bytes = need;
         }
         a.ws = p->ws;
-        e = vtb::launch_reg_path(a);
+        e = vtb::launch_k7_global(a);
     } else if (want_lds && vtb::lds_path_supported(a)) {
         e = vtb::launch_lds_path(a);
     } else {
@@ -250,6 +263,11 @@ int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input
     p->L = frame_bits;
     p->T = frame_bits + code->constraint_length - 1;
     p->device = device;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            p->cus = cus;
+    }
     edge_table(code, p->symm);
     // Shape check up front so a plan that exists can always launch.
     vtb::Launch a;
@@ -257,7 +275,7 @@ int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input
     a.soft = input == VTB_INPUT_SOFT8;
     a.T = p->T;
     a.L = p->L;
-    if (!vtb::k7_lds_supported(a) && !vtb::reg_path_supported(a) && !vtb::lds_path_supported(a)) {
+    if (!vtb::k7_lds_supported(a) && !vtb::k7_global_supported(a) && !vtb::lds_path_supported(a)) {
         delete p;
         return VTB_ERR_UNSUPPORTED;
     }

@@ -45,10 +45,11 @@ bool k7_lds_supported(const Launch& a);
 size_t k7_lds_bytes(const Launch& a);
 hipError_t launch_k7_lds(const Launch& a);
 
-// K=7, survivors in a global workspace (vtb_reg_path.hip): long frames.
-bool reg_path_supported(const Launch& a);
-size_t reg_path_workspace_bytes(const Launch& a);
-hipError_t launch_reg_path(const Launch& a);
+// K=7, the same kernel with survivor words in a global workspace (vtb_k7_lds.hip): long
+// frames, and frames whose LDS survivors would cut the occupancy.
+bool k7_global_supported(const Launch& a);
+size_t k7_global_workspace_bytes(const Launch& a);
+hipError_t launch_k7_global(const Launch& a);
 
 // Stream-ordered scratch memory from a per-device pool that keeps its memory (no release
 // back to the driver between launches), so a per-launch workspace costs no hipMalloc.

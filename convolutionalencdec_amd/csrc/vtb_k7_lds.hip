@@ -149,7 +149,8 @@ __host__ __device__ __forceinline__ uint32_t rev6(uint32_t l) {
 // and each window is one read, one shift and one bit-field insert on the address.
 // Returns the 48 decoded bits with bit 0 = step tlo (a sextet's bits are its end location
 // in l' numbering, oldest step at bit 0).
-__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4) {
+template <bool GS>
+__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t gbase) {
     uint32_t a = cb | l4;
     uint64_t bits = 0;
 #pragma unroll
@@ -158,7 +159,12 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4) {
         if (j % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - j / 3));  // sextet end tlo + todd + 1
         const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);      // window's bits in its half-word
         uint32_t v;  // survivor half-word (smem is LDS address 0: dynamic LDS only)
-        asm volatile("ds_read_u16 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"((todd >> 4) * 256));
+        if constexpr (GS) {
+            asm volatile("global_load_ushort %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * 256));
+        } else {
+            asm volatile("ds_read_u16 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"((todd >> 4) * 256));
+        }
         const int pos = 2 + (todd - 1) % 6;  // address bit of l' bit (t_even mod 6)
         const uint32_t fld = pos >= sh ? (v << (pos - sh)) : (v >> (sh - pos));
         a = (a & ~(3u << pos)) | (fld & (3u << pos));
@@ -199,10 +205,27 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 #define VTB_EXP_WORD(x) x
 #endif
 
-template <bool SOFT>
+// Survivor word W (of the chunk's three) of this lane: LDS store, or a global store at
+// byte offset gvo + 256 W of the wave's workspace (one coalesced 256-B wave store).
+template <bool GS>
+__device__ __forceinline__ void store_word(uint32_t* dchunk, uint32_t gvo, uint64_t gbase, int W, uint32_t z) {
+    if constexpr (GS) {
+        if (W == 0) asm volatile("global_store_dword %0, %1, %2" ::"v"(gvo), "v"(z), "s"(gbase) : "memory");
+        if (W == 1) asm volatile("global_store_dword %0, %1, %2 offset:256" ::"v"(gvo), "v"(z), "s"(gbase) : "memory");
+        if (W == 2) asm volatile("global_store_dword %0, %1, %2 offset:512" ::"v"(gvo), "v"(z), "s"(gbase) : "memory");
+    } else {
+        dchunk[W * 64] = z;
+    }
+}
+
+// GS = false: survivor words in LDS at [r0, r0 + 16 Tpad).  GS = true: survivor words in a
+// global workspace, 16 Tpad bytes per wave at ws + blockIdx.x * ws_wave (same addressing with
+// r0 = 0), for frames whose survivors do not fit in LDS or would cut the occupancy.
+template <bool SOFT, bool GS>
 __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
-                                                    int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table) {
+                                                    int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
+                                                    uint8_t* __restrict__ ws, size_t ws_wave) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
     extern __shared__ uint4 smem4[];
@@ -212,6 +235,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const int lane = threadIdx.x;
     const size_t fa = (size_t)blockIdx.x * 2, fb = fa + 1;
     const bool has_b = fb < frames;
+    const uint64_t gbase = GS ? uniform64(reinterpret_cast<uint64_t>(ws + blockIdx.x * ws_wave)) : 0;
     const uint8_t* inA = in + fa * in_stride;
     const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
 
@@ -247,11 +271,17 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     };
     // Row values of the lane's step: e[c] = 4e(c) and et[c] = 4e(c) + tie (tie bit b = t & 1
     // in both halves).  Branch-free, so the compiler can interleave it with ACS steps.
-    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4]) {
+    // first: no survivor stores outstanding.  In the loop (GS) one survivor-word store (step
+    // 15 of the chunk) was issued after the loads; vmcnt retires in issue order.
+    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4], bool first) {
 #ifdef VTB_EXP_RAWNOWAIT
         ra = lane * 0x0101u, rb = lane * 0x0303u;  // measurement only: no wait for the loads
 #else
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+        if (GS && !first) {
+            asm volatile("s_waitcnt vmcnt(1)" : "+v"(ra), "+v"(rb));
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+        }
 #endif
         // packed [frame A, frame B] received values of coded bits 0 and 1, times four
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
@@ -294,7 +324,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     };
     auto stage = [&](int c, uint32_t ra, uint32_t rb) {
         uint32_t e[4], et[4];
-        stage_compute(ra, rb, e, et);
+        stage_compute(ra, rb, e, et, true);
         stage_write(c, e, et);
     };
 
@@ -320,6 +350,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
         uint32_t* dchunk = dec + (t0 >> 4) * 64 + widx;
+        const uint32_t gvo = 4u * ((t0 >> 4) * 64 + widx);  // GS: byte offset of the lane's words
 
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
@@ -342,14 +373,14 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
                 z = bfi_op(0x0F0F0F0Fu, z, pw[2] << 4);                                          \
                 z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
-                VTB_EXP_WORD(dchunk[((I) >> 4) * 64] = z);                                       \
+                VTB_EXP_WORD(store_word<GS>(dchunk, gvo, gbase, ((I) >> 4), z));                  \
             }                                                                                    \
         }                                                                                        \
     }
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
         if ((G) == 0) load_raw(c0 + 1, ra, rb);                                                   \
-        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set);                            \
+        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set, false);                            \
         if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
             stage_write(c0 + 1, se, set);                                                         \
         }                                                                                         \
@@ -367,12 +398,13 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 #undef VTB_STEP
 #undef VTB_RD
     }
+    if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
     if (dbg & 1) return;
 
     // ---------------- traceback: verified block-parallel chains ----------------
     const int f = lane >> 5, blk = lane & 31;
-    const uint32_t cb0 = uint32_t(r0 + 2 * f);  // this frame's 16-bit half of the word columns
+    const uint32_t cb0 = uint32_t((GS ? 0 : r0) + 2 * f);  // this frame's 16-bit half of the word columns
     uint8_t* ob = tab + f * 4 * tbb;                                      // decoded bytes, index t/8
     const int top = (blk + 1) * tbb;
     const int start_full = top + kTbWarm;
@@ -384,7 +416,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {  // lane's walk has begun (start is a multiple of 48)
-            const uint64_t bits = tb_body(cb0 + 256 * (tlo >> 4), loc);
+            const uint64_t bits = tb_body<GS>(cb0 + 256 * (tlo >> 4), loc, gbase);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
@@ -406,7 +438,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb_body(cb0 + 256 * (tlo >> 4), loc));
+                put_bits48(ob, tlo, tb_body<GS>(cb0 + 256 * (tlo >> 4), loc, gbase));
             }
             fin = loc;
             fixed = true;
@@ -432,25 +464,60 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     }
 }
 
-}  // namespace
+// LDS of the survivor-in-global variant: table ring and decoded bytes only.
+size_t lds_bytes_gs(int T) { return (size_t)region0(T); }
+size_t ws_wave_bytes(int T) { return 16 * (size_t)t_pad(T); }
+constexpr size_t kMaxWsBytes = size_t(1) << 30;  // workspace per launch slab
 
-bool k7_lds_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes(a.T) <= 160 * 1024; }
+// Waves (frame pairs) per launch of the global variant: the whole batch, unless its
+// workspace would exceed kMaxWsBytes; then the batch runs as several launches over one
+// workspace (stream-ordered).
+size_t slab_waves(const Launch& a) {
+    const size_t waves = (a.frames + 1) / 2;
+    size_t slab = kMaxWsBytes / ws_wave_bytes(a.T);
+    if (slab < 1) slab = 1;
+    return slab < waves ? slab : waves;
+}
 
-size_t k7_lds_bytes(const Launch& a) { return lds_bytes(a.T); }
-
-hipError_t launch_k7_lds(const Launch& a) {
+template <bool GS>
+hipError_t launch_k7(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
-    const size_t lds = lds_bytes(a.T);
-    auto kern = a.soft ? k7_lds_kernel<true> : k7_lds_kernel<false>;
+    if (GS && !a.ws) return hipErrorInvalidValue;
+    const size_t lds = GS ? lds_bytes_gs(a.T) : lds_bytes(a.T);
+    auto kern = a.soft ? k7_lds_kernel<true, GS> : k7_lds_kernel<false, GS>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
     const size_t waves = (a.frames + 1) / 2;
-    hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), a);
-    return hipGetLastError();
+    const size_t slab = GS ? slab_waves(a) : waves;
+    const int dbg = debug_flags();
+    for (size_t w0 = 0; w0 < waves; w0 += slab) {
+        const size_t nw = waves - w0 < slab ? waves - w0 : slab;
+        const size_t f0 = 2 * w0;
+        const size_t nf = a.frames - f0 < 2 * nw ? a.frames - f0 : 2 * nw;
+        hipLaunchKernelGGL(kern, dim3(unsigned(nw)), dim3(64), lds, a.stream, a.in + f0 * a.in_stride, a.in_stride,
+                           a.out + f0 * a.out_stride, a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T),
+                           nf, dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
+
+}  // namespace
+
+bool k7_lds_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes(a.T) <= 160 * 1024; }
+
+size_t k7_lds_bytes(const Launch& a) { return lds_bytes(a.T); }
+
+hipError_t launch_k7_lds(const Launch& a) { return launch_k7<false>(a); }
+
+bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T) <= 160 * 1024; }
+
+size_t k7_global_workspace_bytes(const Launch& a) { return slab_waves(a) * ws_wave_bytes(a.T); }
+
+hipError_t launch_k7_global(const Launch& a) { return launch_k7<true>(a); }
 
 }  // namespace vtb

@@ -10,7 +10,7 @@
 // the LDS survivor words from state 0.
 //
 // This is the simple, obviously-correct kernel: the register-resident kernel
-// (vtb_reg_path.hip) is the fast path; this one also covers every K in 3..9.
+// (vtb_k7_lds.hip) is the fast path; this one also covers every K in 3..9.
 //
 // Metric arithmetic (DESIGN.md "Metric formulation"): centred integer metrics.  For
 // butterfly j with trellis label c = symm[j] and received pair (q0, q1) (hard: bits,

@@ -16,7 +16,8 @@ torch = pytest.importorskip("torch")
 from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, native  # noqa: E402
 
 # "auto": the library's own choice; the others force one kernel family: "k7" (K=7,
-# survivors in LDS), "gws" (K=7, survivors in a global workspace), "lds" (every K).
+# survivors in LDS), "gws" (the same K=7 kernel with survivors in a global workspace), "lds"
+# (every K).
 KERNELS = ("auto", "k7", "gws", "lds")
 
 
@@ -95,6 +96,23 @@ def test_soft_random_vs_oracle(orc, K, L, kernel):
         expect = orc.decode(K, CODES[K], q, L, soft=True)
         got = dev_decode(ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True), q)
         assert (got == expect).all(), (K, L, sigma)
+
+
+@pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("L", [10000, 16384])
+def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
+    """Frames past the LDS-resident kernel's survivor capacity up to the API maximum
+    (VTB_MAX_FRAME_BITS, reference viterbiDecoder.h:18): the global-survivor variant."""
+    K = 7
+    kernel.need(K)
+    if kernel == "k7" or (kernel == "lds" and soft and L == 16384):
+        pytest.skip("survivors of this frame length exceed one CU's LDS for this kernel family")
+    if soft:
+        unc, x = random_frames(orc, K, L, 67, 0.0, 31 + L, soft=True, sigma=0.6287)
+    else:
+        unc, x = random_frames(orc, K, L, 67, 0.05, 31 + L)
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    assert (dev_decode(d, x) == orc.decode(K, CODES[K], x, L, soft=soft)).all()
 
 
 def test_soft_extreme_values(orc, kernel):

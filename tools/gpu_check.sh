@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 for s in $steps; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/gpu_tests.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
       rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
       [ $rc -eq 0 ] || exit $rc ;;
     smoke)
