@@ -2,8 +2,8 @@
 // host/device entry points and the multi-GPU shard driver.
 //
 // Host-side only; the trellis work happens in the kernels of vtb_k7_lds.hip (K=7, the fast
-// path, survivors in LDS or, for long frames, in a global workspace) and vtb_lds_path.hip
-// (every K).
+// path, survivors in LDS or, for long frames, in a global workspace), vtb_k9.hip (K=9) and
+// vtb_lds_path.hip (every K).
 
 #include <hip/hip_runtime.h>
 
@@ -85,7 +85,7 @@ bool env_flag_is(const char* name, const char* value) {
     return v && std::strcmp(v, value) == 0;
 }
 
-// Which kernel family a plan uses (see below).  VTB_KERNEL=k7|gws|lds forces one (testing
+// Which kernel family a plan uses (see below).  VTB_KERNEL=k7|gws|k9|lds forces one (testing
 // and A/B measurement); a forced kernel that does not support the shape is an error.
 int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
            size_t frames, hipStream_t stream) {
@@ -106,6 +106,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     const bool want_k7 = any || env_flag_is("VTB_KERNEL", "k7");
     const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
     const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
+    const bool want_k9 = any || env_flag_is("VTB_KERNEL", "k9");
     hipError_t e;
     // K=7: survivors in LDS while that LDS leaves the CU as many waves (2 frames each) as
     // the batch can give it, up to 2 per SIMD (the ACS is VALU-bound there: more waves do
@@ -120,22 +121,29 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
         const size_t fit = (160 * 1024) / vtb::k7_lds_bytes(a);
         k7_in_lds = !any || fit >= want || !vtb::k7_global_supported(a);
     }
-    if (k7_in_lds) {
-        e = vtb::launch_k7_lds(a);
-    } else if (want_gws && vtb::k7_global_supported(a)) {
-        const size_t need = vtb::k7_global_workspace_bytes(a);
+    // plan-owned workspace (survivor words), grown on demand
+    auto workspace = [&](size_t need) -> bool {
         if (need > p->ws_bytes) {
             if (p->ws) (void)vtb::workspace_free(p->ws, stream);
             p->ws = nullptr;
             p->ws_bytes = 0;
             if (vtb::workspace_alloc(&p->ws, need, stream) != hipSuccess) {
                 p->ws = nullptr;
-                return VTB_ERR_NOMEM;
+                return false;
             }
             p->ws_bytes = need;
         }
         a.ws = p->ws;
+        return true;
+    };
+    if (k7_in_lds) {
+        e = vtb::launch_k7_lds(a);
+    } else if (want_gws && vtb::k7_global_supported(a)) {
+        if (!workspace(vtb::k7_global_workspace_bytes(a))) return VTB_ERR_NOMEM;
         e = vtb::launch_k7_global(a);
+    } else if (want_k9 && vtb::k9_supported(a)) {
+        if (!workspace(vtb::k9_workspace_bytes(a))) return VTB_ERR_NOMEM;
+        e = vtb::launch_k9(a);
     } else if (want_lds && vtb::lds_path_supported(a)) {
         e = vtb::launch_lds_path(a);
     } else {
@@ -275,7 +283,8 @@ int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input
     a.soft = input == VTB_INPUT_SOFT8;
     a.T = p->T;
     a.L = p->L;
-    if (!vtb::k7_lds_supported(a) && !vtb::k7_global_supported(a) && !vtb::lds_path_supported(a)) {
+    if (!vtb::k7_lds_supported(a) && !vtb::k7_global_supported(a) && !vtb::k9_supported(a) &&
+        !vtb::lds_path_supported(a)) {
         delete p;
         return VTB_ERR_UNSUPPORTED;
     }

@@ -51,6 +51,11 @@ bool k7_global_supported(const Launch& a);
 size_t k7_global_workspace_bytes(const Launch& a);
 hipError_t launch_k7_global(const Launch& a);
 
+// K=9, survivors in a global workspace (vtb_k9.hip).
+bool k9_supported(const Launch& a);
+size_t k9_workspace_bytes(const Launch& a);
+hipError_t launch_k9(const Launch& a);
+
 // Stream-ordered scratch memory from a per-device pool that keeps its memory (no release
 // back to the driver between launches), so a per-launch workspace costs no hipMalloc.
 hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream);

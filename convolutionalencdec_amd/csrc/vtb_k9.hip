@@ -1,0 +1,461 @@
+// K=9 (256 states) decoder, hard and 8-bit soft input: BASELINE config C4.
+//
+// The K=7 kernel's design (vtb_k7_lds.hip header) scaled to 256 states:
+//
+// Layout.  One wave64 decodes two frames, A and B, packed in the u16 halves of every
+// register.  Location l (8 bits) = r * 64 + lambda lives in register M[r] of lane
+// lane_of(lambda): location bits 0..5 are lane bits (lane XOR 1, 2, 7, 8, 16, 32 through
+// the same involution as K=7), bits 6..7 select one of four registers.
+//
+// In-place state relabelling (reference butterfly viterbiDecoderButterflyk1.c:101-152).
+// Location l holds state rotl8(l, t mod 8) at step t; the two sources of a butterfly sit
+// at locations differing in bit p = 7 - (t mod 8).  For p = 7, 6 the partner is another
+// register of the same lane (no cross-lane op at all); for p = 5, 4 an in-place
+// v_permlane32/16_swap per register; for p = 3..0 a DPP row_ror:8 / row_half_mirror /
+// quad_perm folded into the add.
+//
+// Metrics carry their decisions exactly as in the K=7 kernel: a stored metric is 4m + h,
+// the tie bit R << b / (1 - R) << b (b = t & 1) enters both candidates from the
+// branch-metric table, so M' = pk_min(A, B) keeps the decision D (the location bit p of
+// the survivor's predecessor) in bit b; after each odd step the two history bits are
+// gathered into per-register survivor words (one v_perm per two windows, three v_bfi per
+// 16 steps) and cleared.  Ties go to the lower predecessor (strict '>', reference
+// :129-130).
+//
+// Start metrics: the reference's K=9 start value is (uint8)(NUM_STATES+1) = 1 (x255 soft,
+// reference viterbiDecoderButterflyk1.c:62), kept exactly (the K=7 kernel's larger
+// equivalent start value does not apply).
+//
+// Renormalisation every 12 steps against location 0 (state 0) with bias B = 16Q (= nQS):
+// for every t, m_t(s) - m_t(0) >= -nQS, and the spread plus 12 steps of growth keeps
+// 4m + 3 + a candidate's table value below 2^16 (DESIGN.md §3, K=9 figures).
+//
+// Survivors.  64 B per step per wave do not fit LDS at useful occupancy, so they go to a
+// per-wave global workspace: per 16 steps a 1-KB column of 256 words, the word of
+// location l at byte 4 rev6(lambda) + 256 rev2(r) -- i.e. address bits 2..7 carry bits
+// 2..7 of l' = rev8(l) and address bits 8..9 its bits 0..1.  Each register's store is one
+// contiguous 256-B wave store.  In l' numbering step t's pairing bit is bit t mod 8, so a
+// window's two decisions are adjacent address bits and the traceback edits the word
+// address in place (one global_load_ushort, one shift, one bit-field insert per window).
+//
+// Frame ends.  Windows pair an even and an odd step, so the kernel runs Tq = T + delta
+// steps with delta = T & 1: for odd T one extra own-keeping step at the start (its table
+// row makes every location keep its own predecessor, which leaves the start metrics
+// unchanged) and the decoded bit stream is shifted back by one bit at the copy-out.  Steps
+// past Tq up to the 48-step chunk grid run on clamped input; afterwards their survivor
+// bits are overwritten with own-keeping decisions, so a walk from location 0 at the end of
+// the padding reaches location 0 (the terminated state) at Tq.
+//
+// Traceback (reference :200-256): the K=7 kernel's verified block-parallel chains, with
+// 8-bit locations (an octet's eight decoded bits are its end location l', oldest step at
+// bit 0).
+
+#include <utility>
+
+#include "vtb_k7_common.h"
+
+namespace vtb {
+namespace {
+
+using k7::pk_min;
+using k7::uniform64;
+
+constexpr int kCh = 48;                  // ACS steps per unrolled chunk (multiple of 8 and 16)
+constexpr int kCol = 49;                 // 8-byte slots per table column (48 rows + bank skew)
+constexpr int kRingBytes = 8 * kCol * 8;  // branch-metric ring: 8 (label, R) columns
+constexpr int kAH = 2;                   // table rows read this many steps ahead
+constexpr int kRS = 3;                   // register ring slots (48 % kRS == 0)
+constexpr int kTbWarm = 48;              // traceback warm-up steps past a block's end
+constexpr uint32_t kR1 = 0x10001u;
+constexpr uint32_t kHist = 0x00030003u;
+constexpr int kColBytes = 1024;          // survivor column: 256 words per 16 steps
+
+int tb_block(int Tq) {
+    const int per = (Tq + 31) / 32;  // 32 blocks per frame, multiple of 48 steps
+    return (per + 47) / 48 * 48;
+}
+int t_pad(int Tq) { return (Tq + kCh - 1) / kCh * kCh; }
+int region0(int Tq) {  // table ring, later the decoded bytes of both frames
+    const int r = 8 * tb_block(Tq) > kRingBytes ? 8 * tb_block(Tq) : kRingBytes;
+    return (r + 255) / 256 * 256;
+}
+size_t ws_wave_bytes(int Tq) { return (size_t)kColBytes * (t_pad(Tq) / 16); }
+
+__device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ (((l >> 2) & 1u) * 3u); }
+__device__ __forceinline__ uint32_t rev6(uint32_t l) {
+    return ((l & 1) << 5) | ((l & 2) << 3) | ((l & 4) << 1) | ((l & 8) >> 1) | ((l & 16) >> 3) | ((l & 32) >> 5);
+}
+__host__ __device__ constexpr int rev2(int r) { return ((r & 1) << 1) | (r >> 1); }
+__device__ __forceinline__ int rotl8(int x, int r) { return ((x << r) | (x >> (8 - r))) & 255; }
+
+__device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+    return r;
+}
+
+// One coalesced wave store of survivor words (saddr form: wave base in SGPRs).
+template <int OFF>
+__device__ __forceinline__ void gstore(uint32_t vo, uint32_t z, uint64_t base) {
+    asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+}
+
+template <int... Is, class F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+
+// Candidates of one step for the four registers: A = own + V, B = partner (across location
+// bit P) + W.
+template <int P>
+__device__ __forceinline__ void candidates(uint32_t (&M)[4], const uint2 (&vw)[4], uint32_t (&A)[4], uint32_t (&B)[4]) {
+    if constexpr (P >= 6) {
+        constexpr int x = 1 << (P - 6);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            A[r] = M[r] + vw[r].x;
+            B[r] = M[r ^ x] + vw[r].y;
+        }
+    } else if constexpr (P == 5 || P == 4) {
+        // The adds separate the last VALU write of each M[r] from its swap; the s_nop the
+        // last swap from the first read of a result (one wait state each way).
+        if constexpr (P == 5) {
+            asm volatile(
+                "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"
+                "v_permlane32_swap_b32 %4, %4\n\tv_permlane32_swap_b32 %5, %5\n\t"
+                "v_permlane32_swap_b32 %6, %6\n\tv_permlane32_swap_b32 %7, %7\n\ts_nop 0"
+                : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3]), "+v"(M[0]), "+v"(M[1]), "+v"(M[2]), "+v"(M[3])
+                : "v"(vw[0].x), "v"(vw[1].x), "v"(vw[2].x), "v"(vw[3].x));
+        } else {
+            asm volatile(
+                "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"
+                "v_permlane16_swap_b32 %4, %4\n\tv_permlane16_swap_b32 %5, %5\n\t"
+                "v_permlane16_swap_b32 %6, %6\n\tv_permlane16_swap_b32 %7, %7\n\ts_nop 0"
+                : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3]), "+v"(M[0]), "+v"(M[1]), "+v"(M[2]), "+v"(M[3])
+                : "v"(vw[0].x), "v"(vw[1].x), "v"(vw[2].x), "v"(vw[3].x));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) B[r] = M[r] + vw[r].y;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            A[r] = M[r] + vw[r].x;
+            if constexpr (P == 3) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x128, 0xF, 0xF, true) + vw[r].y;  // row_ror:8
+            if constexpr (P == 2) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x141, 0xF, 0xF, true) + vw[r].y;  // XOR 7
+            if constexpr (P == 1) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x4E, 0xF, 0xF, true) + vw[r].y;   // XOR 2
+            if constexpr (P == 0) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0xB1, 0xF, 0xF, true) + vw[r].y;   // XOR 1
+        }
+    }
+}
+
+// Address bit of l' bit e inside a survivor column (bits 2..7 in place, bits 0..1 at 8..9).
+__host__ __device__ constexpr int addr_pos(int e) { return e >= 2 ? e : e + 8; }
+__device__ __forceinline__ uint32_t lprime_of(uint32_t a) { return (a & 0xFCu) | ((a >> 8) & 3u); }
+
+// 48 traceback steps over [tlo, tlo + 48), newest first (see vtb_k7_lds.hip tb_body).  cb is
+// the byte offset of the block's first survivor column plus 2f (bits 2..9 clear); la the
+// address field of the survivor's location.  Returns the 48 decoded bits, bit 0 = step tlo.
+__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t gbase) {
+    uint32_t a = cb | la;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 24; j++) {
+        const int todd = 47 - 2 * j;
+        if (j % 4 == 0) bits |= uint64_t(lprime_of(a)) << (8 * (5 - j / 4));  // octet ending at tlo + todd + 1
+        const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+        uint32_t v;
+        asm volatile("global_load_ushort %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                     : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * kColBytes));
+        const int pos = addr_pos((todd - 1) & 7);
+        const uint32_t fld = pos >= sh ? (v << (pos - sh)) : (v >> (sh - pos));
+        a = (a & ~(3u << pos)) | (fld & (3u << pos));
+    }
+    la = a & 0x3FCu;
+    return bits;
+}
+
+__device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) {
+    unsigned short* o = reinterpret_cast<unsigned short*>(ob + (tlo >> 3));
+    const uint32_t r = __builtin_bitreverse32(uint32_t(bits)), rh = __builtin_bitreverse32(uint32_t(bits >> 32));
+    o[0] = (unsigned short)((r >> 24) | ((r >> 8) & 0xff00u));
+    o[1] = (unsigned short)(((r >> 8) & 0xffu) | ((r & 0xffu) << 8));
+    o[2] = (unsigned short)((rh >> 24) | ((rh >> 8) & 0xff00u));
+}
+
+template <bool SOFT>
+__global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
+                                                int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
+                                                uint8_t* __restrict__ ws, size_t ws_wave) {
+    constexpr uint32_t Q = SOFT ? 255 : 1;
+    constexpr uint32_t B4 = 4 * 16 * Q;  // renormalised metric of location 0, times four
+    extern __shared__ uint4 smem4[];
+    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
+    const int lane = threadIdx.x;
+    const size_t fa = (size_t)blockIdx.x * 2, fb = fa + 1;
+    const bool has_b = fb < frames;
+    const uint8_t* inA = in + fa * in_stride;
+    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;
+    const uint64_t gbase = uniform64(reinterpret_cast<uint64_t>(ws + blockIdx.x * ws_wave));
+    const uint32_t lam = lane_of(lane);  // this lane's 6 low location bits
+
+    // Per register and phase: byte offset of the (V, W) column (edge label c of the
+    // butterfly's upper state, R = bit p of the location).
+    uint32_t off[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int ph = 0; ph < 8; ph++) {
+            const int l = r * 64 + int(lam), p = 7 - ph;
+            off[r][ph] = 8u * kCol * (table.symm[rotl8(l & ~(1 << p), ph)] + 4u * ((l >> p) & 1u));
+        }
+
+    // Table staging (as vtb_k7_lds.hip): lane r < 48 builds ring row r of a chunk from the
+    // raw input of kernel step 48c + r, i.e. input step 48c + r - delta.
+    const int srow = lane < kCh ? lane : lane - kCh;
+    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA)), baseB = uniform64(reinterpret_cast<uint64_t>(inB));
+    auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
+        int t = c * kCh + srow - delta;
+        t = t < 0 ? 0 : (t < T ? t : T - 1);
+        if constexpr (SOFT) {
+            asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
+                         : "=&v"(ra), "=&v"(rb) : "v"(2u * uint32_t(t)), "s"(baseA), "s"(baseB));
+        } else {
+            asm volatile("global_load_ubyte %0, %2, %3\n\tglobal_load_ubyte %1, %2, %4"
+                         : "=&v"(ra), "=&v"(rb) : "v"(uint32_t(t)), "s"(baseA), "s"(baseB));
+        }
+    };
+    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4]) {
+        uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
+        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
+        if constexpr (!SOFT) {
+            q1 = (q0 >> 1) & kR1;
+            q0 &= kR1;
+        }
+        q0 <<= 2;
+        q1 <<= 2;
+        constexpr uint32_t QQ = 4 * Q * kR1;
+        e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
+        const uint32_t tie = (1u + (srow & 1)) * kR1;
+#pragma unroll
+        for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
+    };
+    // Column k = c + 4R holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
+    const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
+    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
+#define VTB_W2(base, k, v, w)                                                                         \
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
+                 "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
+        VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
+        VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
+        VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+#undef VTB_W2
+        if (c == 0 && srow < delta) {  // the own-keeping start step (odd T)
+            uint2* col = reinterpret_cast<uint2*>(tab) + srow;
+            constexpr uint32_t PADW = 4 * (2 * Q + 1) * kR1;
+            const uint32_t tie = et[0] - e[0];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                col[k * kCol] = make_uint2(0u, PADW + tie);
+                col[(4 + k) * kCol] = make_uint2(tie, PADW);
+            }
+        }
+    };
+
+    uint32_t M[4];
+    M[0] = (lane == 0) ? B4 * kR1 : (B4 + 4 * Q) * kR1;
+    M[1] = M[2] = M[3] = (B4 + 4 * Q) * kR1;
+    uint32_t ra, rb;
+    {
+        uint32_t e[4], et[4];
+        load_raw(0, ra, rb);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+        stage_compute(ra, rb, e, et);
+        stage_write(0, e, et);
+    }
+    uint2 buf[kRS][4];
+#pragma unroll
+    for (int s = 0; s < kAH; s++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) buf[s][r] = *reinterpret_cast<const uint2*>(tab + off[r][s] + 8 * s);
+
+    const uint32_t wlane = 4u * rev6(lam);  // survivor word byte offset of the lane within a column
+    uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4];
+    const int tacs = (dbg & 2) ? 0 : Tpad;
+    for (int t0 = 0; t0 < tacs; t0 += kCh) {
+        const int c0 = t0 / kCh;
+        const uint32_t gvo = uint32_t(kColBytes) * uint32_t(t0 >> 4) + wlane;
+        static_for(std::make_integer_sequence<int, kCh>{}, [&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            constexpr int PH = I % 8;
+            if constexpr (I == 0) load_raw(c0 + 1, ra, rb);  // next chunk's raw input
+            if constexpr (I == 20) {
+                // one survivor store batch (step 15) was issued after the loads
+                asm volatile("s_waitcnt vmcnt(4)" : "+v"(ra), "+v"(rb));
+                stage_compute(ra, rb, se, set);
+            }
+            if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);  // all rows of this chunk read
+            if constexpr ((I % 12) == 10) {
+                const uint32_t ref = __builtin_amdgcn_readfirstlane(M[0]);
+                asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(B4 * kR1), "s"(ref) : "scc");
+            }
+            uint32_t A[4], Bc[4];
+            candidates<7 - PH>(M, buf[I % kRS], A, Bc);
+            // table rows kAH steps ahead (ring row (I + kAH) % 48: next chunk's rows wrap)
+            {
+                constexpr int IN = (I + kAH) % kCh, PN = IN % 8;
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    buf[(I + kAH) % kRS][r] = *reinterpret_cast<const uint2*>(tab + off[r][PN] + 8 * IN);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) M[r] = pk_min(A[r], Bc[r]);
+            if constexpr (I & 1) {
+                constexpr int w = (I & 15) >> 1;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    if constexpr (w & 1) pw[r][w >> 1] = __builtin_amdgcn_perm(M[r], m_prev[r], 0x06020400u);
+                    else m_prev[r] = M[r];
+                    M[r] = ((I % 12) == 11) ? ((M[r] & ~kHist) + dd) : (M[r] & ~kHist);
+                }
+                if constexpr ((I & 15) == 15) {
+                    constexpr int W = I >> 4;
+                    uint32_t z[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        z[r] = bfi_op(0x03030303u, pw[r][0], pw[r][1] << 2);
+                        z[r] = bfi_op(0x0F0F0F0Fu, z[r], pw[r][2] << 4);
+                        z[r] = bfi_op(0x3F3F3F3Fu, z[r], pw[r][3] << 6);
+                    }
+                    gstore<W * kColBytes + 256 * rev2(0)>(gvo, z[0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(1)>(gvo, z[1], gbase);
+                    gstore<W * kColBytes + 256 * rev2(2)>(gvo, z[2], gbase);
+                    gstore<W * kColBytes + 256 * rev2(3)>(gvo, z[3], gbase);
+                }
+            }
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // Padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping decisions
+    // (both history bits = the location's own bits t_even mod 8, +1 of l').
+    if (!(dbg & 2)) {
+        uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + blockIdx.x * ws_wave);
+        for (int g = Tq >> 4; g < (Tpad >> 4); g++) {
+            const int w0 = Tq > 16 * g ? (Tq - 16 * g) >> 1 : 0;  // first padding window of the word
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint32_t lp = (rev6(lam) << 2) | uint32_t(rev2(r));
+                uint32_t own = 0, mask = 0;
+                for (int w = w0; w < 8; w++) {
+                    const int sh = 8 * (w & 1) + 2 * (w >> 1);
+                    own |= ((lp >> (2 * (w & 3))) & 3u) << sh;
+                    mask |= 3u << sh;
+                }
+                own |= own << 16;
+                mask |= mask << 16;
+                uint32_t* p = wsw + (kColBytes / 4) * g + (wlane >> 2) + 64 * rev2(r);
+                *p = (*p & ~mask) | (own & mask);
+            }
+        }
+    }
+    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (dbg & 1) return;
+
+    // ---------------- traceback: verified block-parallel chains (vtb_k7_lds.hip) ----------------
+    const int f = lane >> 5, blk = lane & 31;
+    const uint32_t cb0 = uint32_t(2 * f);
+    uint8_t* ob = tab + f * 4 * tbb;
+    const int top = (blk + 1) * tbb;
+    const int start_full = top + kTbWarm;
+    const int start = min(start_full, Tpad);
+    const bool known = start >= Tq;
+    const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;
+    uint32_t loc = 0, loc_top = 0;
+    for (int g = 0; g < nbody; g++) {
+        const int tlo = start_full - 48 * (g + 1);
+        if (g == kTbWarm / 48) loc_top = loc;
+        if (tlo < start) {
+            const uint64_t bits = tb_body(cb0 + kColBytes * (tlo >> 4), loc, gbase);
+            if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
+        }
+    }
+    uint32_t fin = loc;
+    bool fixed = known || (dbg & 4);
+    for (int round = 0; round < 33; round++) {
+        const uint32_t sf = __shfl_down(fin, 1);
+        const bool ok = fixed || loc_top == sf;
+        const uint64_t bad = ~__ballot(ok);
+        if (bad == 0) break;
+        const uint32_t badf = uint32_t(bad >> (32 * f));
+        const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+        if (!ok && succ_proven) {
+            loc = sf;
+            for (int g = kTbWarm / 48; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                put_bits48(ob, tlo, tb_body(cb0 + kColBytes * (tlo >> 4), loc, gbase));
+            }
+            fin = loc;
+            fixed = true;
+        }
+    }
+    __syncthreads();
+
+    // copy out; with delta = 1 kernel step t' is input step t' - 1 (shift the stream one bit)
+    const int nbytes = (L + 7) >> 3;
+    for (int i = lane; i < 2 * nbytes; i += 64) {
+        const int fr = i >= nbytes, j = i - fr * nbytes;
+        if (fr && !has_b) break;
+        const uint8_t* s = tab + fr * 4 * tbb;
+        const uint8_t v = delta ? uint8_t((s[j] << 1) | (s[j + 1] >> 7)) : s[j];
+        out[(fr ? fb : fa) * out_stride + j] = v;
+    }
+}
+
+size_t slab_waves(const Launch& a, int Tq) {
+    const size_t waves = (a.frames + 1) / 2;
+    size_t slab = (size_t(1) << 30) / ws_wave_bytes(Tq);
+    if (slab < 1) slab = 1;
+    return slab < waves ? slab : waves;
+}
+
+}  // namespace
+
+bool k9_supported(const Launch& a) {
+    return a.S == 8 && a.T > a.S && (size_t)region0(a.T + (a.T & 1)) <= 160 * 1024;
+}
+
+size_t k9_workspace_bytes(const Launch& a) {
+    const int Tq = a.T + (a.T & 1);
+    return slab_waves(a, Tq) * ws_wave_bytes(Tq);
+}
+
+hipError_t launch_k9(const Launch& a) {
+    if (a.frames == 0) return hipSuccess;
+    if (!a.ws) return hipErrorInvalidValue;
+    const int delta = a.T & 1, Tq = a.T + delta;
+    const size_t lds = (size_t)region0(Tq);
+    auto kern = a.soft ? k9_kernel<true> : k9_kernel<false>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+    }
+    const size_t waves = (a.frames + 1) / 2;
+    const size_t slab = slab_waves(a, Tq);
+    const int dbg = debug_flags();
+    for (size_t w0 = 0; w0 < waves; w0 += slab) {
+        const size_t nw = waves - w0 < slab ? waves - w0 : slab;
+        const size_t f0 = 2 * w0;
+        const size_t nf = a.frames - f0 < 2 * nw ? a.frames - f0 : 2 * nw;
+        hipLaunchKernelGGL(kern, dim3(unsigned(nw)), dim3(64), lds, a.stream, a.in + f0 * a.in_stride, a.in_stride,
+                           a.out + f0 * a.out_stride, a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), nf,
+                           dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace vtb

@@ -16,15 +16,17 @@ torch = pytest.importorskip("torch")
 from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, native  # noqa: E402
 
 # "auto": the library's own choice; the others force one kernel family: "k7" (K=7,
-# survivors in LDS), "gws" (the same K=7 kernel with survivors in a global workspace), "lds"
-# (every K).
-KERNELS = ("auto", "k7", "gws", "lds")
+# survivors in LDS), "gws" (the same K=7 kernel with survivors in a global workspace), "k9"
+# (K=9, survivors in a global workspace), "lds" (every K).
+KERNELS = ("auto", "k7", "gws", "k9", "lds")
 
 
 class Kern(str):
     def need(self, K):
         if self in ("k7", "gws") and K != 7:
             pytest.skip(f"kernel {self} is K=7 only")
+        if self == "k9" and K != 9:
+            pytest.skip("kernel k9 is K=9 only")
 
 
 @pytest.fixture(scope="module")
@@ -76,7 +78,7 @@ def test_soft_bridge_golden_vectors(K, kernel):
 @pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000])
 def test_hard_random_vs_oracle(orc, K, g, L, kernel):
     kernel.need(K)
-    if L > 4096 and K not in (5, 7):
+    if L > 4096 and K not in (5, 7) and (kernel == "lds" or K != 9):
         pytest.skip("survivor memory of this K and L exceeds one CU's LDS (DESIGN.md, frame-length limits)")
     for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
         unc, rx = random_frames(orc, K, L, 257, p, seed + L, g=g)
@@ -115,9 +117,27 @@ def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
     assert (dev_decode(d, x) == orc.decode(K, CODES[K], x, L, soft=soft)).all()
 
 
-def test_soft_extreme_values(orc, kernel):
+@pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("L", [4095, 16384])
+def test_k9_long_frames_vs_oracle(orc, L, soft, kernel):
+    """K=9 frames up to the API maximum (reference viterbiDecoder.h:18), odd and even T."""
+    K = 9
+    kernel.need(K)
+    if kernel == "lds" and L > 4096:
+        pytest.skip("survivors of this frame length exceed one CU's LDS for the generic kernel")
+    if soft:
+        unc, x = random_frames(orc, K, L, 33, 0.0, 41 + L, soft=True, sigma=0.6287)
+    else:
+        unc, x = random_frames(orc, K, L, 33, 0.04, 41 + L)
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    assert (dev_decode(d, x) == orc.decode(K, CODES[K], x, L, soft=soft)).all()
+
+
+@pytest.mark.parametrize("K", [7, 9])
+def test_soft_extreme_values(orc, K, kernel):
     """Saturated, constant and alternating soft inputs (tie-heavy) match the oracle."""
-    K, L = 7, 512
+    kernel.need(K)
+    L = 512
     T = L + K - 1
     rng = np.random.default_rng(7)
     cases = [np.zeros((4, T, 2), np.uint8), np.full((4, T, 2), 255, np.uint8), np.full((4, T, 2), 128, np.uint8),
@@ -130,6 +150,7 @@ def test_soft_extreme_values(orc, kernel):
 def test_bertest_k7_kat_on_gpu(orc, kernel):
     """The reference berTestK7 stream (glibc rand seed 9865, 3 x 10000 packets) decoded on
     the GPU gives exactly the reference's decoded bit-error counts."""
+    kernel.need(7)
     unc, rx, _ = orc.bertest()
     d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=2048)
     for c in range(3):
