@@ -85,8 +85,18 @@ constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) c
 #endif
 constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
 constexpr uint32_t kR1 = 0x10001u;
-constexpr uint32_t kHist = 0x00030003u;  // history bits of both frames
-constexpr uint32_t kBias4 = 4 * 3060;    // renormalised metric of location 0, times four
+
+// History bits per u16 half: soft input keeps 4m + h (2 history bits, the
+// exact metric needs 14 bits); hard input, whose metrics stay below 128, keeps 256m + h
+// with 8 history bits (tie bit at t mod 8, clear and survivor byte every 8 steps, eight
+// decisions per traceback read).
+template <bool SOFT>
+struct Hist {
+    static constexpr int HB = SOFT ? 2 : 8;                  // history bits
+    static constexpr uint32_t SC = 1u << HB;                 // metric scale
+    static constexpr uint32_t MASK = (SC - 1) * 0x10001u;    // history bits of both frames
+    static constexpr uint32_t BIAS = SC * (SOFT ? 3060 : 12);  // renormalised location-0 metric (scaled)
+};
 
 int tb_block(int T) {
     const int per = (T + 31) / 32;  // 32 blocks per frame, multiple of 48 steps
@@ -173,6 +183,37 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t 
     return bits;
 }
 
+__device__ __forceinline__ uint32_t rotl6c(uint32_t x, int r) { return r == 0 ? x : ((x << r) | (x >> (6 - r))) & 63u; }
+__device__ __forceinline__ uint32_t rotr6c(uint32_t x, int r) { return r == 0 ? x : ((x >> r) | (x << (6 - r))) & 63u; }
+
+// Hard input (8 history bits): 48 traceback steps as six octets, one byte read each.  The
+// byte of octet k (steps tlo + 8k + b, b = 0..7) at the survivor's location holds the
+// decisions D_b along its path; D_b replaces l' bit r_b = (8k + b) mod 6, so the location
+// eight steps back is rotl6(byte & 63, r_0) (bits b = 6, 7 are overwritten by b = 0, 1) and
+// the decoded bits are [byte bit 6, byte bit 7, u2, u3, u4, u5, u0, u1] with
+// u = rotr6(end location l', r_0).
+template <bool GS>
+__device__ __forceinline__ uint64_t tb_body8(uint32_t cb, uint32_t& l4, uint64_t gbase) {
+    uint32_t a = cb | l4;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int k = 5; k >= 0; k--) {
+        const int r0 = (8 * k) % 6;
+        const uint32_t u = rotr6c((a >> 2) & 63u, r0);
+        uint32_t v;
+        if constexpr (GS) {
+            asm volatile("global_load_ubyte %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"(256 * (k >> 1) + (k & 1)));
+        } else {
+            asm volatile("ds_read_u8 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"(256 * (k >> 1) + (k & 1)));
+        }
+        bits |= uint64_t((u & 0x3Cu) | ((v >> 6) & 3u) | ((u & 3u) << 6)) << (8 * k);
+        a = (a & ~0xFCu) | (rotl6c(v & 63u, r0) << 2);
+    }
+    l4 = a & 0xFCu;
+    return bits;
+}
+
 // Output bytes of steps [tlo, tlo + 48) (bit 0 of bits = step tlo; bytes MSB-first as the
 // reference packs them, viterbiDecoderButterflyk1.c:243-249).
 __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) {
@@ -191,8 +232,16 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 #endif
 #ifdef VTB_EXP_NO_TABREAD
 #define VTB_EXP_TABREAD(rd, reg) make_uint2((reg).y, (reg).x)
+#elif defined(VTB_EXP_TAB32)
+// measurement only: read V alone (4 B per lane) and derive W = (8Q + tie) - V at use
+#define VTB_EXP_TABREAD(rd, reg) make_uint2(reinterpret_cast<const uint32_t*>(&(rd))[0], 0u)
 #else
 #define VTB_EXP_TABREAD(rd, reg) (rd)
+#endif
+#ifdef VTB_EXP_TAB32
+#define VTB_EXP_VW(vw, I) make_uint2((vw).x, (8 * Q + (1u << ((I) & (H::HB - 1)))) * kR1 - (vw).x)
+#else
+#define VTB_EXP_VW(vw, I) (vw)
 #endif
 #ifdef VTB_EXP_NO_STAGE
 #define VTB_EXP_STAGE false
@@ -228,6 +277,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ ws, size_t ws_wave) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
+    using H = Hist<SOFT>;
     extern __shared__ uint4 smem4[];
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem4);
     uint8_t* tab = smem;
@@ -290,12 +340,12 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             q1 = (q0 >> 1) & kR1;
             q0 &= kR1;
         }
-        q0 <<= 2;
-        q1 <<= 2;
+        q0 <<= H::HB;
+        q1 <<= H::HB;
         // 4e of labels 0..3 (bit 0 of a label <-> coded bit 0); halves never borrow
-        constexpr uint32_t QQ = 4 * Q * kR1;
+        constexpr uint32_t QQ = H::SC * Q * kR1;
         e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
-        const uint32_t tie = (1u + (srow & 1)) * kR1;
+        const uint32_t tie = (1u << (srow & (H::HB - 1))) * kR1;
 #pragma unroll
         for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
     };
@@ -313,7 +363,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
 #undef VTB_W2
         if ((c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows (last chunk only)
-            constexpr uint32_t PADW = 4 * (12 * Q + 1) * kR1;
+            constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -328,7 +378,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         stage_write(c, e, et);
     };
 
-    uint32_t M = (lane == 0) ? kBias4 * kR1 : (kBias4 + 4 * INIT) * kR1;
+    uint32_t M = (lane == 0) ? H::BIAS * kR1 : (H::BIAS + H::SC * INIT) * kR1;
     uint32_t ra, rb;
     load_raw(0, ra, rb);
     stage(0, ra, rb);
@@ -352,22 +402,25 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         uint32_t* dchunk = dec + (t0 >> 4) * 64 + widx;
         const uint32_t gvo = 4u * ((t0 >> 4) * 64 + widx);  // GS: byte offset of the lane's words
 
+// Renormalisation: reference = location 0 (lane 0) at a step whose history is clear, the
+// subtraction folded into the history clear (soft: every 12 steps; hard: once per chunk).
+#define VTB_RENORM_READ(I) (SOFT ? ((I) % 12) == 10 : (I) == 40)
+#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % 12) == 11 : (I) == 47)
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
-        if (((I) % 12) == 10) {                                                                  \
-            /* renormalisation reference: location 0 (lane 0), history clear at this point */    \
+        if (VTB_RENORM_READ(I)) {                                                                \
             const uint32_t ref = __builtin_amdgcn_readfirstlane(M);                              \
-            asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(kBias4 * kR1), "s"(ref) : "scc");        \
+            asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(H::BIAS * kR1), "s"(ref) : "scc");       \
         }                                                                                        \
         uint32_t A, B;                                                                           \
-        candidates<5 - (PH)>(M, cur[PH], A, B);                                                  \
+        candidates<5 - (PH)>(M, VTB_EXP_VW(cur[PH], I), A, B);                                   \
         M = pk_min(A, B);                                                                        \
-        if ((I) & 1) {                                                                           \
+        if (SOFT && ((I) & 1)) {                                                                 \
             /* window (I) >> 1 & 7 of the word: history bytes of two windows by one v_perm */    \
             const int w = ((I) & 15) >> 1;                                                       \
             if (w & 1) pw[w >> 1] = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
             else m_prev = M;                                                                     \
-            M = (((I) % 12) == 11) ? ((M & ~kHist) + dd) : (M & ~kHist);                         \
+            M = VTB_RENORM_APPLY(I) ? ((M & ~H::MASK) + dd) : (M & ~H::MASK);                    \
             if (((I) & 15) == 15) {                                                              \
                 /* bits 2j..2j+1 of byte (w & 1): window w = 2j + (w & 1) */                     \
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
@@ -375,6 +428,16 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
                 z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
                 VTB_EXP_WORD(store_word<GS>(dchunk, gvo, gbase, ((I) >> 4), z));                  \
             }                                                                                    \
+        }                                                                                        \
+        if (!SOFT && ((I) & 7) == 7) {                                                           \
+            /* octet history bytes: [A oct 0, A oct 1, B oct 0, B oct 1] per 16 steps */         \
+            if (((I) & 15) == 7) {                                                               \
+                m_prev = M;                                                                      \
+            } else {                                                                             \
+                const uint32_t z = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
+                VTB_EXP_WORD(store_word<GS>(dchunk, gvo, gbase, ((I) >> 4), z));                  \
+            }                                                                                    \
+            M = VTB_RENORM_APPLY(I) ? ((M & ~H::MASK) + dd) : (M & ~H::MASK);                    \
         }                                                                                        \
     }
 #define VTB_GROUP(G)                                                                              \
@@ -396,6 +459,8 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
+#undef VTB_RENORM_READ
+#undef VTB_RENORM_APPLY
 #undef VTB_RD
     }
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
@@ -411,12 +476,16 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const int start = min(start_full, Tpad);
     const bool known = start >= T;  // walk starts on the known path (location 0 at and past T)
     const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;  // dbg bit 3: warm-up walk only
+    auto tb48 = [&](uint32_t cb, uint32_t& l4) {
+        if constexpr (SOFT) return tb_body<GS>(cb, l4, gbase);
+        else return tb_body8<GS>(cb, l4, gbase);
+    };
     uint32_t loc = 0, loc_top = 0;  // survivor location as 4 l'
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {  // lane's walk has begun (start is a multiple of 48)
-            const uint64_t bits = tb_body<GS>(cb0 + 256 * (tlo >> 4), loc, gbase);
+            const uint64_t bits = tb48(cb0 + 256 * (tlo >> 4), loc);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
@@ -438,7 +507,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb_body<GS>(cb0 + 256 * (tlo >> 4), loc, gbase));
+                put_bits48(ob, tlo, tb48(cb0 + 256 * (tlo >> 4), loc));
             }
             fin = loc;
             fixed = true;

@@ -7,7 +7,7 @@ build() {
   name=$1; shift
   d=convolutionalencdec_amd/lib/exp/$name; mkdir -p $d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -I$CS "$@" \
-      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_gen.hip
+      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_k9.hip $CS/vtb_gen.hip
 }
 for v in "$@"; do
   case $v in
@@ -23,6 +23,8 @@ for v in "$@"; do
     warm96) build warm96 -DVTB_EXP_TBWARM=96 ;;
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
+    base) build base ;;
+    tab32) build tab32 -DVTB_EXP_TAB32 ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
