@@ -78,8 +78,8 @@ class Timer:
         for _ in range(steps):
             step()
         self.sync()
+        dt = time.perf_counter() - t0  # this rank's K steps; the closing barrier is not timed
         self.barrier()
-        dt = time.perf_counter() - t0
         return self.allreduce_max(dt)
 
 
@@ -138,6 +138,21 @@ def load_traffic(workload_key):
             return json.load(fh).get(workload_key)
     except (OSError, ValueError):
         return None
+
+
+def load_valu(workload_key):
+    """VALU wave-instructions per launch from the rocprofv3 SQ pass (profiles/pmc_valu.json)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_valu.json")) as fh:
+            return json.load(fh).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 integer VALU instruction per 4 cycles per
+# SIMD (v_add_u32 / v_pk_min_u16 / DPP adds: tools/probes/isa_bench.hip, profiles/r01), at the
+# 2.4 GHz peak engine clock.
+VALU_PEAK_G = 256 * 4 * 2.4 / 4
 
 
 def main():
@@ -202,14 +217,15 @@ def main():
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
     elapsed = timer.run(step, args.steps)
 
-    # Per-launch device time with HIP events on the launch stream (roofline numerator).
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in ev:
-        a.record(stream)
+    # Average launch duration with HIP events on the launch stream (roofline numerator): one
+    # event pair around K back-to-back launches, as rocprofv3's per-kernel average sees them.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        b.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     ms_per_step = elapsed / args.steps * 1e3
     total_bits = F * L * world
@@ -219,6 +235,14 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload_key = f"K{code[0]}_{'soft' if soft else 'hard'}_F{F}_L{L}"
     traffic = load_traffic(workload_key)
+    valu = load_valu(workload_key)
+    secondary = {"bound": "valu", "state_steps_per_s": round(F * (1 << (code[0] - 1)) * T / (kern_ms * 1e-3)),
+                 "note": "packed u16 ACS, 2 frames per wave64; see DESIGN.md 5"}
+    if valu:
+        ach = valu["valu_wave_insts_per_launch"] / (kern_ms * 1e-3) / 1e9
+        secondary.update({"achieved": round(ach, 2), "peak": VALU_PEAK_G, "unit": "G wave64-VALU-instr/s",
+                          "frac": round(ach / VALU_PEAK_G, 4),
+                          "valu_wave_insts_per_launch": valu["valu_wave_insts_per_launch"]})
 
     if rank != 0:
         if world > 1:
@@ -260,8 +284,7 @@ def main():
             "kernel_ms": round(kern_ms, 5),
             "algorithmic_bytes_per_launch": alg_bytes,
             # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)
-            "secondary": {"bound": "valu", "state_steps_per_s": round(F * (1 << (code[0] - 1)) * T / (kern_ms * 1e-3)),
-                          "note": "packed u16 ACS, 2 frames per wave64; see DESIGN.md 5"},
+            "secondary": secondary,
         },
         "cpu_baseline": cpu,
     }

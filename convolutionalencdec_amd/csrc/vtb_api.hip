@@ -38,6 +38,22 @@ struct vtb_plan {
     int cus = 256;  // compute units of the device (kernel choice)
 };
 
+// Streaming decoder (include/viterbi_amd.h "Streaming decode"): all streams advance in
+// lockstep, so the step counters live here; per-stream emission state is on the device.
+struct vtb_stream {
+    vtb_code_t code;
+    vtb_input_t input;
+    size_t streams = 0;
+    int ring = 0;  // survivor ring per wave, steps (multiple of 48)
+    int device = 0;
+    uint8_t symm[1 << (vtb::kMaxS - 1)];
+    uint32_t* d_state = nullptr;  // waves x kStreamStateWords
+    uint8_t* d_carry = nullptr;   // streams x kStreamCarryStride
+    void* d_ring = nullptr;       // waves x 16 * ring bytes
+    int t_begin = 0;              // steps decoded in the current frame (multiple of 48)
+    int carry_len = 0;            // segments received but not yet decoded (< 48)
+};
+
 namespace {
 
 int parity(uint64_t x) { return __builtin_popcountll(x) & 1; }
@@ -377,6 +393,122 @@ int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
     for (auto& t : th) t.join();
     for (int r : rc)
         if (r != VTB_OK) return r;
+    return VTB_OK;
+}
+
+int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t input, size_t streams,
+                      int32_t window_steps, int device) {
+    if (!sp) return VTB_ERR_INVALID;
+    *sp = nullptr;
+    int e = check_code(code);
+    if (e != VTB_OK) return e;
+    if (code->constraint_length != 7) return VTB_ERR_UNSUPPORTED;
+    if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
+    if (streams == 0 || streams > (size_t(1) << 31)) return VTB_ERR_INVALID;
+    const int64_t win = window_steps <= 0 ? 49152 : (int64_t(window_steps) + 47) / 48 * 48;
+    if (win < 96 || win > (int64_t(1) << 27)) return VTB_ERR_INVALID;  // 16 B per step: 32-bit ring offsets
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return VTB_ERR_DEVICE;
+    if (!device_is_gfx950(device)) return VTB_ERR_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    vtb_stream* s = new (std::nothrow) vtb_stream();
+    if (!s) return VTB_ERR_NOMEM;
+    s->code = *code;
+    s->input = input;
+    s->streams = streams;
+    s->ring = int(win);
+    s->device = device;
+    edge_table(code, s->symm);
+    const size_t waves = (streams + 1) / 2;
+    if (hipMalloc(&s->d_state, waves * vtb::kStreamStateWords * 4) != hipSuccess ||
+        hipMalloc(&s->d_carry, streams * vtb::kStreamCarryStride) != hipSuccess ||
+        hipMalloc(&s->d_ring, waves * 16 * size_t(s->ring)) != hipSuccess) {
+        vtb_stream_destroy(s);
+        return VTB_ERR_NOMEM;
+    }
+    if (hipMemset(s->d_state, 0, waves * vtb::kStreamStateWords * 4) != hipSuccess) {
+        vtb_stream_destroy(s);
+        return VTB_ERR_DEVICE;
+    }
+    *sp = s;
+    return VTB_OK;
+}
+
+void vtb_stream_destroy(vtb_stream_t* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    (void)hipDeviceSynchronize();  // calls on any stream may still use the buffers
+    if (s->d_state) (void)hipFree(s->d_state);
+    if (s->d_carry) (void)hipFree(s->d_carry);
+    if (s->d_ring) (void)hipFree(s->d_ring);
+    delete s;
+}
+
+size_t vtb_stream_out_bytes(const vtb_stream_t* s) { return s ? size_t(s->ring) / 8 + 8 : 0; }
+
+int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, int32_t segments, int last,
+                      uint8_t* d_out, size_t out_stride, int32_t* d_out_bits, void* stream) {
+    if (!s || segments < 0 || !d_out || !d_out_bits || (segments > 0 && !d_in)) return VTB_ERR_INVALID;
+    const int sb = s->input == VTB_INPUT_SOFT8 ? 2 : 1;
+    if (segments > 0 && in_stride < size_t(segments) * sb) return VTB_ERR_INVALID;
+    if (out_stride < vtb_stream_out_bytes(s)) return VTB_ERR_INVALID;
+    if (segments > s->ring - 48) return VTB_ERR_INVALID;
+    const int rows = s->carry_len + segments;  // < ring
+    const int64_t T = int64_t(s->t_begin) + rows;
+    if (T > int64_t(1) << 30) return VTB_ERR_UNSUPPORTED;
+    if (last && T < s->code.constraint_length) return VTB_ERR_INVALID;  // a frame needs L >= 1
+    const int nproc = last ? (rows + 47) / 48 * 48 : rows / 48 * 48;
+    const int t_end = s->t_begin + nproc;
+    DeviceGuard g(s->device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    if (!last && nproc == 0) {
+        // nothing to decode yet: no bits this call
+        if (hipMemsetAsync(d_out_bits, 0, s->streams * sizeof(int32_t), hs) != hipSuccess) return VTB_ERR_DEVICE;
+    } else {
+        vtb::Launch a;
+        a.S = s->code.constraint_length - 1;
+        a.soft = sb == 2;
+        a.T = int(T);
+        a.L = int(T) - a.S;
+        a.in = d_in;
+        a.in_stride = in_stride;
+        a.out = d_out;
+        a.out_stride = out_stride;
+        a.frames = s->streams;
+        a.stream = hs;
+        a.ws = s->d_ring;
+        std::memcpy(a.symm, s->symm, sizeof(a.symm));
+        vtb::StreamArgs sa;
+        sa.state = s->d_state;
+        sa.carry = s->d_carry;
+        sa.carry_len = s->carry_len;
+        sa.t_begin = s->t_begin;
+        sa.t_end = t_end;
+        sa.last = last ? 1 : 0;
+        sa.ring = s->ring;
+        sa.out_bits = d_out_bits;
+        if (vtb::launch_k7_stream(a, sa) != hipSuccess) return VTB_ERR_DEVICE;
+    }
+    // rows received past the last whole 48-step chunk wait in the carry for the next call
+    const int leftover = last ? 0 : rows - nproc;
+    if (leftover > 0) {
+        const int first = rows - leftover;  // first leftover row: in the carry only if nothing was decoded
+        const uint8_t* src = nproc == 0 ? d_in : d_in + size_t(first - s->carry_len) * sb;
+        uint8_t* dst = s->d_carry + size_t(nproc == 0 ? s->carry_len : 0) * sb;
+        const int width = (nproc == 0 ? segments : leftover) * sb;
+        if (width > 0 && hipMemcpy2DAsync(dst, vtb::kStreamCarryStride, src, in_stride, size_t(width), s->streams,
+                                          hipMemcpyDeviceToDevice, hs) != hipSuccess)
+            return VTB_ERR_DEVICE;
+    }
+    if (last) {
+        s->t_begin = 0;
+        s->carry_len = 0;
+    } else {
+        s->t_begin = t_end;
+        s->carry_len = leftover;
+    }
     return VTB_OK;
 }
 

@@ -51,6 +51,26 @@ bool k7_global_supported(const Launch& a);
 size_t k7_global_workspace_bytes(const Launch& a);
 hipError_t launch_k7_global(const Launch& a);
 
+// K=7 streaming decode (vtb_stream_*, include/viterbi_amd.h): the global-survivor variant of
+// the K=7 kernel continued across launches.  All streams of one stream object advance in
+// lockstep, so the step counters are host-side; what depends on the data (how far each
+// stream has emitted) lives in the per-wave state.  Launch::T is the steps received so far
+// (t_begin + carry_len + new segments), Launch::in the call's new rows, Launch::ws the
+// survivor ring.
+constexpr int kStreamStateWords = 68;   // per wave: M[64] (packed metric pairs), e[2], flags, pad
+constexpr int kStreamCarryStride = 96;  // per stream: up to 47 held-back segments (2 B soft)
+struct StreamArgs {
+    uint32_t* state = nullptr;       // waves x kStreamStateWords
+    const uint8_t* carry = nullptr;  // streams x kStreamCarryStride
+    int carry_len = 0;               // rows in the carry at the call (< 48)
+    int t_begin = 0;                 // steps decoded by earlier calls (multiple of 48)
+    int t_end = 0;                   // steps decoded after this call (multiple of 48)
+    int last = 0;                    // terminate: traceback from state 0 at step T
+    int ring = 0;                    // survivor ring per wave in steps (multiple of 48)
+    int32_t* out_bits = nullptr;     // per stream: bits emitted by this call, -1 = window overflow
+};
+hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s);
+
 // K=9, survivors in a global workspace (vtb_k9.hip).
 bool k9_supported(const Launch& a);
 size_t k9_workspace_bytes(const Launch& a);

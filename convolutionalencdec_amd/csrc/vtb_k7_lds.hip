@@ -267,14 +267,124 @@ __device__ __forceinline__ void store_word(uint32_t* dchunk, uint32_t gvo, uint6
     }
 }
 
+// Decoded bits of steps [tlo, tlo + 48) to global memory at o (byte stores: a stream row
+// has no alignment guarantee).
+__device__ __forceinline__ void put_bits48_global(uint8_t* o, uint64_t bits) {
+    const uint32_t r = __builtin_bitreverse32(uint32_t(bits)), rh = __builtin_bitreverse32(uint32_t(bits >> 32));
+    o[0] = uint8_t(r >> 24), o[1] = uint8_t(r >> 16), o[2] = uint8_t(r >> 8), o[3] = uint8_t(r);
+    o[4] = uint8_t(rh >> 24), o[5] = uint8_t(rh >> 16);
+}
+
+// Traceback of one streaming call (vtb_stream_decode).  Frame f of the wave has emitted the
+// decoded bits of steps [0, e_f) before the call.
+//  * Not last: walks from all 64 locations at t_end go back 48 steps at a time until they
+//    stand on one location (step m).  Every survivor path then passes through it, so no
+//    later input can change the path below m: the bits of [e_f, m) are final -- equal to
+//    the whole-frame decode's, hence the reference's -- and are emitted.  m <= t_end - 48,
+//    so the zero tail (the last K - 1 steps of a frame) is never emitted early.
+//  * Last: the terminated traceback from location 0 at T (the padding rows keep location 0,
+//    as in the frame decoder) emits [e_f, T - 6).
+// The emission is the frame decoder's verified block-parallel traceback over [e_f, hi) with
+// all 64 lanes on one frame, entering at the location known at hi.  If the ring no longer
+// holds step e_f (no merge within sa.ring steps) the frame is flagged: -1 bits until last.
+template <bool SOFT>
+__device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
+                                 uint64_t gbase, size_t fa, bool has_b) {
+    const int lane = threadIdx.x;
+    uint32_t* st = sa.state + size_t(blockIdx.x) * kStreamStateWords;
+    int e[2] = {int(__builtin_amdgcn_readfirstlane(st[64])), int(__builtin_amdgcn_readfirstlane(st[65]))};
+    uint32_t flags = __builtin_amdgcn_readfirstlane(st[66]);
+    auto tb48 = [&](int tlo, int f, uint32_t& l4) -> uint64_t {
+        const uint32_t cb = uint32_t(2 * f + 256 * ((tlo % sa.ring) >> 4));
+        if constexpr (SOFT) return tb_body<true>(cb, l4, gbase);
+        else return tb_body8<true>(cb, l4, gbase);
+    };
+    for (int f = 0; f < 2; f++) {
+        if (f == 1 && !has_b) break;
+        const int e0 = e[f];
+        int bits_out;
+        if (((flags >> f) & 1u) || t_end - e0 > sa.ring) {
+            flags |= 1u << f;
+            bits_out = -1;
+        } else {
+            int hi = e0, kfrom = e0;
+            uint32_t kloc = 0;
+            if (sa.last) {
+                hi = t_end, kfrom = T;
+            } else {
+                uint32_t l4 = 4u * uint32_t(lane);  // every location (l' = lane)
+                for (int tlo = t_end - 48; tlo >= e0; tlo -= 48) {
+                    (void)tb48(tlo, f, l4);
+                    const uint32_t l0 = __builtin_amdgcn_readfirstlane(l4);
+                    if (__all(l4 == l0)) {
+                        hi = kfrom = tlo, kloc = l0;
+                        break;
+                    }
+                }
+            }
+            if (hi > e0) {
+                const int n = hi - e0;                              // multiple of 48
+                const int tbb = ((n + 63) / 64 + 47) / 48 * 48;     // 64 blocks of whole sextet-octets
+                const int bot = e0 + lane * tbb;
+                const bool active = bot < hi;
+                const int start_full = bot + tbb + kTbWarm;
+                const int start = min(start_full, hi);
+                const bool known = start >= kfrom;
+                const int nbody = (kTbWarm + tbb) / 48;
+                uint8_t* ob = out + (fa + f) * out_stride;  // byte (tlo - e0) / 8 of the call's bits
+                uint32_t loc = known ? kloc : 0u, loc_top = loc;
+                if (active) {
+                    for (int g = 0; g < nbody; g++) {
+                        const int tlo = start_full - 48 * (g + 1);
+                        if (g == kTbWarm / 48) loc_top = loc;
+                        if (tlo < start) {
+                            const uint64_t bits = tb48(tlo, f, loc);
+                            if (g >= kTbWarm / 48) put_bits48_global(ob + ((tlo - e0) >> 3), bits);
+                        }
+                    }
+                }
+                // verification, as in the frame decoder (one frame over 64 blocks)
+                uint32_t fin = loc;
+                bool fixed = known || !active;
+                for (int round = 0; round < 65; round++) {
+                    const uint32_t sf = __shfl_down(fin, 1);
+                    const bool ok = fixed || loc_top == sf;
+                    const uint64_t bad = ~__ballot(ok);
+                    if (bad == 0) break;
+                    const bool succ_proven = lane == 63 || (bad >> (lane + 1)) == 0;
+                    if (!ok && succ_proven) {
+                        loc = sf;
+                        for (int g = kTbWarm / 48; g < nbody; g++) {
+                            const int tlo = start_full - 48 * (g + 1);
+                            put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, f, loc));
+                        }
+                        fin = loc;
+                        fixed = true;
+                    }
+                }
+            }
+            bits_out = sa.last ? T - 6 - e0 : hi - e0;
+            e[f] = hi;
+        }
+        if (lane == 0) sa.out_bits[fa + f] = bits_out;
+    }
+    if (sa.last) e[0] = e[1] = 0, flags = 0;  // the streams restart with the next frame
+    if (lane == 0) st[64] = uint32_t(e[0]), st[65] = uint32_t(e[1]), st[66] = flags;
+}
+
 // GS = false: survivor words in LDS at [r0, r0 + 16 Tpad).  GS = true: survivor words in a
 // global workspace, 16 Tpad bytes per wave at ws + blockIdx.x * ws_wave (same addressing with
 // r0 = 0), for frames whose survivors do not fit in LDS or would cut the occupancy.
-template <bool SOFT, bool GS>
+// STREAM (with GS): one call of the streaming decoder (vtb_stream_decode): steps
+// [sa.t_begin, Tpad = sa.t_end) continue from the metrics in sa.state, survivor words go to a
+// ring of sa.ring steps, and the traceback emits the bits that became final (see
+// stream_traceback below).
+template <bool SOFT, bool GS, bool STREAM>
 __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
-                                                    uint8_t* __restrict__ ws, size_t ws_wave) {
+                                                    uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
+    static_assert(GS || !STREAM, "the streaming decoder keeps its survivors in a global ring");
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
     using H = Hist<SOFT>;
@@ -311,7 +421,22 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         const int t = c * kChunk + srow;
         const uint32_t tc = uint32_t(t < T ? t : T - 1);
-        if constexpr (SOFT) {
+        if constexpr (STREAM) {
+            // row r of this call: the carry's held-back rows first, then the new input
+            constexpr int SB = SOFT ? 2 : 1;
+            const int r = int(tc) - sa.t_begin;
+            const uint8_t* pa = r < sa.carry_len ? sa.carry + fa * kStreamCarryStride + SB * r
+                                                 : inA + SB * (r - sa.carry_len);
+            const uint8_t* pb = r < sa.carry_len ? sa.carry + (has_b ? fb : fa) * kStreamCarryStride + SB * r
+                                                 : inB + SB * (r - sa.carry_len);
+            if constexpr (SOFT) {
+                asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off"
+                             : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            } else {
+                asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
+                             : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            }
+        } else if constexpr (SOFT) {
             asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
                          : "=&v"(ra), "=&v"(rb) : "v"(2 * tc), "s"(baseA), "s"(baseB));
         } else {
@@ -379,9 +504,16 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     };
 
     uint32_t M = (lane == 0) ? H::BIAS * kR1 : (H::BIAS + H::SC * INIT) * kR1;
-    uint32_t ra, rb;
-    load_raw(0, ra, rb);
-    stage(0, ra, rb);
+    // first step of this launch: 0, or (streaming) where the previous call stopped
+    const int tbeg = STREAM ? sa.t_begin : 0;
+    if constexpr (STREAM) {
+        if (tbeg > 0) M = sa.state[size_t(blockIdx.x) * kStreamStateWords + lane];
+    }
+    uint32_t ra = 0, rb = 0;
+    if (!STREAM || Tpad > tbeg) {  // (a streaming call may have no new step)
+        load_raw(tbeg / kChunk, ra, rb);
+        stage(tbeg / kChunk, ra, rb);
+    }
     // software pipeline: the table pairs of group G+3 are read while group G computes, into
     // the slot of a four-group register ring (8 groups per chunk: no copies at the loop edge)
     uint2 buf[4][6];
@@ -394,13 +526,14 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
     const int tacs = (dbg & 2) ? 0 : Tpad;
-    for (int t0 = 0; t0 < tacs; t0 += kChunk) {
+    for (int t0 = tbeg; t0 < tacs; t0 += kChunk) {
         const int c0 = t0 / kChunk;
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
         uint32_t* dchunk = dec + (t0 >> 4) * 64 + widx;
-        const uint32_t gvo = 4u * ((t0 >> 4) * 64 + widx);  // GS: byte offset of the lane's words
+        // GS: byte offset of the lane's words (streaming: position in the survivor ring)
+        const uint32_t gvo = 4u * (((STREAM ? t0 % sa.ring : t0) >> 4) * 64 + widx);
 
 // Renormalisation: reference = location 0 (lane 0) at a step whose history is clear, the
 // subtraction folded into the history clear (soft: every 12 steps; hard: once per chunk).
@@ -465,6 +598,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     }
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
+    if constexpr (STREAM) {
+        if (!sa.last) sa.state[size_t(blockIdx.x) * kStreamStateWords + lane] = M;
+        stream_traceback<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b);
+        return;
+    }
     if (dbg & 1) return;
 
     // ---------------- traceback: verified block-parallel chains ----------------
@@ -553,7 +691,7 @@ hipError_t launch_k7(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (GS && !a.ws) return hipErrorInvalidValue;
     const size_t lds = GS ? lds_bytes_gs(a.T) : lds_bytes(a.T);
-    auto kern = a.soft ? k7_lds_kernel<true, GS> : k7_lds_kernel<false, GS>;
+    auto kern = a.soft ? k7_lds_kernel<true, GS, false> : k7_lds_kernel<false, GS, false>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -568,7 +706,7 @@ hipError_t launch_k7(const Launch& a) {
         const size_t nf = a.frames - f0 < 2 * nw ? a.frames - f0 : 2 * nw;
         hipLaunchKernelGGL(kern, dim3(unsigned(nw)), dim3(64), lds, a.stream, a.in + f0 * a.in_stride, a.in_stride,
                            a.out + f0 * a.out_stride, a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T),
-                           nf, dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T));
+                           nf, dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -588,5 +726,19 @@ bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_
 size_t k7_global_workspace_bytes(const Launch& a) { return slab_waves(a) * ws_wave_bytes(a.T); }
 
 hipError_t launch_k7_global(const Launch& a) { return launch_k7<true>(a); }
+
+// One streaming call: every wave (two streams) continues its trellis over [s.t_begin,
+// s.t_end) and emits the final bits (stream_traceback).  LDS: the table ring only.
+hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s) {
+    if (a.frames == 0) return hipSuccess;
+    if (!a.ws || !s.state || !s.out_bits || s.ring < 48 || s.ring % 48 || s.t_begin % 48 || s.t_end % 48)
+        return hipErrorInvalidValue;
+    auto kern = a.soft ? k7_lds_kernel<true, true, true> : k7_lds_kernel<false, true, true>;
+    const size_t lds = (kRingBytes + 255) / 256 * 256;
+    const size_t waves = (a.frames + 1) / 2;
+    hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
+                       a.T, a.L, s.t_end, 0, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring), s);
+    return hipGetLastError();
+}
 
 }  // namespace vtb

@@ -6,6 +6,9 @@ Reference (C, compile-time configured)                 here (runtime configured)
   viterbiInitButterflyk1()     ...Butterflyk1.c:8-44     ConvCode.edge_table()
   VITERBI_DECODER_HARD(st, coded, out, T, last=true)     ViterbiDecoder.decode(frames)
       ...Butterflyk1.c:82-263   (one frame per call)        (a batch of frames per call)
+  VITERBI_DECODER_HARD(st, chunk, out, n, last=false/true) ViterbiStream.push(chunks, last)
+      ...Butterflyk1.c:85-196   (state kept across calls)   (a batch of streams per call,
+                                                              bits emitted once final)
 
 `decode` takes either a torch uint8 tensor already on a ROCm device (decoded on that
 device, on torch's current stream, no host round trip) or a host numpy array (copied in
@@ -124,6 +127,71 @@ class ViterbiDecoder:
         except ImportError:  # pragma: no cover
             pass
         return self.decode_host(frames)
+
+
+class ViterbiStream:
+    """Streaming decoder over the C ABI (vtb_stream_*; K=7): `streams` independent streams
+    advancing in lockstep on one device.  push(chunk, last) feeds `segments` more coded
+    segments per stream (torch uint8 tensor on the device, [streams, segments] hard or
+    [streams, segments, 2] / [streams, 2*segments] soft) and returns (bytes, nbits): row i of
+    `bytes` holds the bits of stream i that became final in this call (MSB-first), nbits[i]
+    their count (-1: window overflow, the frame is lost).  The concatenated bits of a frame
+    equal ViterbiDecoder.decode of the whole frame.  last=True ends the frame."""
+
+    def __init__(self, code=ConvCode(), streams=1, soft=False, window_steps=0, device=0):
+        self.code = code if isinstance(code, ConvCode) else ConvCode(*code)
+        self.streams = int(streams)
+        self.soft = bool(soft)
+        self.device = int(device)
+        L = native.lib()
+        c = self.code._c()
+        h = ctypes.c_void_p()
+        native.check(
+            L.vtb_stream_create(ctypes.byref(h), ctypes.byref(c),
+                                native.VTB_INPUT_SOFT8 if self.soft else native.VTB_INPUT_HARD, self.streams,
+                                int(window_steps), self.device),
+            "vtb_stream_create")
+        self._h = h
+        self.out_bytes = int(L.vtb_stream_out_bytes(h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            native.lib().vtb_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, chunk, last=False, stream=None):
+        import torch
+
+        sb = 2 if self.soft else 1
+        dev = torch.device("cuda", self.device)
+        if chunk is None:
+            x = torch.empty((self.streams, 0), dtype=torch.uint8, device=dev)
+        else:
+            if chunk.dtype != torch.uint8 or not chunk.is_cuda:
+                raise TypeError("push expects a torch.uint8 tensor on a ROCm device")
+            x = chunk.reshape(self.streams, -1)
+            if x.stride(1) != 1:
+                x = x.contiguous()
+        if x.shape[1] % sb:
+            raise ValueError("soft input needs two bytes per segment")
+        segs = x.shape[1] // sb
+        out = torch.empty((self.streams, self.out_bytes), dtype=torch.uint8, device=dev)
+        nbits = torch.empty(self.streams, dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        in_ptr = ctypes.c_void_p(x.data_ptr()) if segs else None
+        native.check(
+            native.lib().vtb_stream_decode(self._h, in_ptr, max(x.stride(0), 1), segs, 1 if last else 0,
+                                           ctypes.c_void_p(out.data_ptr()), out.stride(0),
+                                           ctypes.c_void_p(nbits.data_ptr()), ctypes.c_void_p(stream)),
+            "vtb_stream_decode")
+        return out, nbits
 
 
 def decode_multi(frames, code=ConvCode(), frame_bits=1024, soft=False, device_mask=0):

@@ -36,6 +36,10 @@ EXPORTED_SYMBOLS = (
     "vtb_decode_host",
     "vtb_decode_host_multi",
     "vtb_decode_frame_legacy",
+    "vtb_stream_create",
+    "vtb_stream_destroy",
+    "vtb_stream_out_bytes",
+    "vtb_stream_decode",
     "vtb_device_count",
     "vtb_rand64",
     "vtb_payload_device",
@@ -98,6 +102,12 @@ def lib():
     L.vtb_decode_host.argtypes = [vp, vp, vp, sz]
     L.vtb_decode_host_multi.argtypes = [cp, ctypes.c_int, i32, vp, vp, sz, ctypes.c_uint32]
     L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
+    L.vtb_stream_create.argtypes = [ctypes.POINTER(vp), cp, ctypes.c_int, sz, i32, ctypes.c_int]
+    L.vtb_stream_destroy.restype = None
+    L.vtb_stream_destroy.argtypes = [vp]
+    L.vtb_stream_out_bytes.restype = sz
+    L.vtb_stream_out_bytes.argtypes = [vp]
+    L.vtb_stream_decode.argtypes = [vp, vp, sz, i32, ctypes.c_int, vp, sz, vp, vp]
     L.vtb_device_count.argtypes = []
     u64 = ctypes.c_uint64
     L.vtb_rand64.restype = u64
@@ -110,7 +120,8 @@ def lib():
     L.vtb_bsc_p32.restype = ctypes.c_uint32
     L.vtb_bsc_p32.argtypes = [ctypes.c_double]
     for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
-                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_device_count", "vtb_payload_device",
+                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_stream_create", "vtb_stream_decode",
+                 "vtb_device_count", "vtb_payload_device",
                  "vtb_encode_device", "vtb_channel_device"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L

@@ -16,6 +16,10 @@
  *                            layout; soft input is the build-defined 8-bit extension)
  *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
  *                           behind include/viterbiDecoder.h (VITERBI_DECODER_HARD)
+ *   vtb_stream_*            the same function called chunk by chunk with last = false and
+ *                           then last = true (:85-196 keep the state across calls), batched
+ *                           over streams, with the block traceback the reference leaves TODO
+ *                           (:195,199)
  *   vtb_encode_device       convEnc                       src/convEncode.c:46-130
  *                           (whole terminated frames, batched on the device)
  *   vtb_payload_device /    the harnesses' random payloads and BSC corruption
@@ -120,6 +124,45 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
 
 /* Number of gfx950 devices visible (0 if none); negative VTB_ERR_DEVICE on runtime error. */
 int vtb_device_count(void);
+
+/* ---- Streaming decode -------------------------------------------------
+ * Replaces the reference's chunked protocol -- viterbiDecoderHardButterflyk1(state, coded,
+ * out, segments, last) called with last = false for each chunk and last = true for the end
+ * of the frame (src/viterbiDecoderButterflyk1.c:82-263) -- for a batch of independent
+ * streams that advance in lockstep on the device, and adds what the reference leaves as
+ * TODO (block traceback with early output, :195,199; src/viterbiDecoder.h:22-25):
+ *   - each call pushes `segments` more coded segments per stream (row i of d_in, same layout
+ *     as a frame's input: 1 byte per segment hard, 2 bytes soft), any count >= 0;
+ *   - bits are emitted as soon as they are final: once the survivor paths of all 64 states
+ *     have merged behind them no later input can change them, so the concatenation of a
+ *     frame's outputs equals the whole-frame decode (vtb_decode_*, the reference's output)
+ *     bit for bit;
+ *   - last != 0 ends the frame: the traceback from state 0 emits the rest (the reference's
+ *     return of (segments - K)/8 + 1 bytes, last byte zero-padded), and every stream starts
+ *     a new frame with the next call.  A frame has at least K segments in total.
+ * Frames are not limited to VTB_MAX_FRAME_BITS: survivors live in a per-stream ring of
+ * `window_steps` trellis steps (rounded up to a multiple of 48; <= 0 selects 49152) in
+ * device memory.  Output bits wait until the paths merge; should a stream go window_steps
+ * steps without a merge (pure-noise input), its frame is lost: d_out_bits reports -1 for it
+ * until the call with last != 0, after which it restarts cleanly.
+ * K = 7 only (VTB_ERR_UNSUPPORTED otherwise); hard or soft input as for plans. */
+typedef struct vtb_stream vtb_stream_t;
+
+int vtb_stream_create(vtb_stream_t** s, const vtb_code_t* code, vtb_input_t input, size_t streams,
+                      int32_t window_steps, int device);
+void vtb_stream_destroy(vtb_stream_t* s);
+
+/* Bytes one call may write per output row (out_stride must be at least this). */
+size_t vtb_stream_out_bytes(const vtb_stream_t* s);
+
+/* One call, asynchronous on `stream` (a hipStream_t; one stream per object, or the caller
+ * orders the calls).  d_in: streams rows of in_stride bytes (>= the segments' bytes); it
+ * must stay valid until the call's work on `stream` completes.  Row i of d_out receives the
+ * call's bits for stream i, MSB-first from bit 0 of byte 0; d_out_bits[i] (device int32)
+ * their count: a multiple of 8 except on the last call of a frame, or -1 (window
+ * overflow).  segments must not exceed window_steps - 48. */
+int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, int32_t segments, int last,
+                      uint8_t* d_out, size_t out_stride, int32_t* d_out_bits, void* stream);
 
 /* ---- Synthetic frames on the device -------------------------------
  * Randomness is one counter-based stream, integer-exact on any host or device:

@@ -96,3 +96,7 @@ def test_plan_without_gpu_fails_loudly():
     out = np.zeros(128, np.uint8)
     assert lib.vtb_decode_frame_legacy(ctypes.byref(c), coded.ctypes.data_as(ctypes.c_void_p), 1030,
                                        out.ctypes.data_as(ctypes.c_void_p)) == native.VTB_ERR_DEVICE
+    stream = ctypes.c_void_p()
+    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(c), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
+    k9 = native.VtbCode.make(9, CODES[9])
+    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k9), 0, 8, 0, 0) == native.VTB_ERR_UNSUPPORTED

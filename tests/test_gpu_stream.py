@@ -1,0 +1,171 @@
+"""GPU parity of the streaming decoder (vtb_stream_*).
+
+The reference decodes a frame pushed in chunks (viterbiDecoderHardButterflyk1 with
+last=false, then last=true; src/viterbiDecoderButterflyk1.c:82-263) exactly as the whole
+frame.  The stream decoder emits bits as soon as they are final, so the contract checked
+here is: for any chunking, the bits a stream emits over a frame's calls, concatenated,
+equal the oracle's whole-frame decode (pinned to the reference's golden vectors) bit for
+bit.  Frames longer than the reference's 16384-bit limit are checked against the oracle's
+unbounded whole-frame decoder."""
+import numpy as np
+import pytest
+
+from helpers import CODES, Oracle, golden_sets, hard_to_soft, random_frames
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, ViterbiStream, native  # noqa: E402
+
+K = 7
+CODE = ConvCode(K, CODES[K])
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+def push_frame(vs, x, sb, chunks):
+    """Push one frame (x: [F, T*sb] uint8 on the device) in `chunks` segments; returns the
+    per-stream emitted bit arrays and the per-call bit counts."""
+    F = x.shape[0]
+    got = [[] for _ in range(F)]
+    counts = []
+    pos = 0
+    for i, c in enumerate(chunks):
+        last = i == len(chunks) - 1
+        piece = x[:, pos * sb:(pos + c) * sb] if c else None
+        out, nb = vs.push(piece, last=last)
+        pos += c
+        out, nb = out.cpu().numpy(), nb.cpu().numpy()
+        counts.append(nb)
+        for f in range(F):
+            if nb[f] > 0:
+                got[f].append(np.unpackbits(out[f])[:nb[f]])
+    assert pos * sb == x.shape[1]
+    return [np.concatenate(g) if g else np.zeros(0, np.uint8) for g in got], np.array(counts)
+
+
+def random_chunks(rng, T, sizes=(1, 7, 47, 48, 49, 96, 100, 333, 1000)):
+    out = []
+    left = T
+    while left > 0:
+        c = int(min(left, rng.choice(sizes)))
+        out.append(c)
+        left -= c
+    if rng.random() < 0.5:
+        out.append(0)  # a last call with no new segments
+    return out
+
+
+def expect_bits(orc, x_host, L, soft):
+    return np.unpackbits(orc.decode(K, CODES[K], x_host, L, soft=soft), axis=1)[:, :L]
+
+
+@pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("L,F", [(1, 3), (42, 4), (1024, 6), (5000, 5)])
+def test_random_chunking_matches_whole_frame(orc, soft, L, F):
+    rng = np.random.default_rng(100 * L + F + soft)
+    if soft:
+        unc, xh = random_frames(orc, K, L, F, 0.0, 7 + L, soft=True, sigma=0.6287)
+    else:
+        unc, xh = random_frames(orc, K, L, F, 0.05, 7 + L)
+    sb = 2 if soft else 1
+    T = L + K - 1
+    x = torch.from_numpy(np.ascontiguousarray(xh).reshape(F, -1)).cuda()
+    vs = ViterbiStream(CODE, streams=F, soft=soft)
+    want = expect_bits(orc, xh, L, soft)
+    for trial in range(3):  # the object restarts after each last call
+        got, counts = push_frame(vs, x, sb, random_chunks(rng, T))
+        for f in range(F):
+            assert got[f].size == L and (got[f] == want[f]).all(), (trial, f)
+        assert (counts[:-1] % 8 == 0).all() and (counts >= 0).all()
+
+
+def test_golden_vectors_streamed(orc):
+    """The reference's golden frames (hard and the soft bridge q = 255*bit) pushed in 100-segment chunks."""
+    for key, L, unc, rx, dec in golden_sets(K):
+        F, T = rx.shape
+        want = np.unpackbits(dec, axis=1)[:, :L]
+        for soft in (False, True):
+            xh = hard_to_soft(rx) if soft else rx
+            x = torch.from_numpy(np.ascontiguousarray(xh).reshape(F, -1)).cuda()
+            vs = ViterbiStream(CODE, streams=F, soft=soft)
+            chunks = [100] * (T // 100) + [T % 100]
+            got, _ = push_frame(vs, x, 2 if soft else 1, chunks)
+            for f in range(F):
+                assert (got[f] == want[f]).all(), (key, soft, f)
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_frames_beyond_reference_limit(orc, soft):
+    """50,000-bit frames (the reference stops at 16384, viterbiDecoder.h:18) in 4096-segment
+    chunks; bits leave the decoder long before the frame ends."""
+    L, F = 50000, 4
+    if soft:
+        unc, xh = random_frames(orc, K, L, F, 0.0, 99, soft=True, sigma=0.5603)
+    else:
+        unc, xh = random_frames(orc, K, L, F, 0.037, 99)
+    T = L + K - 1
+    x = torch.from_numpy(np.ascontiguousarray(xh).reshape(F, -1)).cuda()
+    vs = ViterbiStream(CODE, streams=F, soft=soft, window_steps=8192)
+    chunks = [4096] * (T // 4096) + [T % 4096]
+    got, counts = push_frame(vs, x, 2 if soft else 1, chunks)
+    want = expect_bits(orc, xh, L, soft)
+    for f in range(F):
+        assert (got[f] == want[f]).all(), f
+    # early output: by the second call every stream has emitted most of what it received
+    assert (counts[1] >= 4096 - 512).all(), counts[1]
+
+
+def test_window_overflow_is_flagged_and_recovers(orc):
+    """Pure-noise input with a 96-step window: streams whose paths do not merge in time
+    report -1 for the rest of the frame; after last every stream decodes the next frame."""
+    F, L = 32, 2000
+    T = L + K - 1
+    rng = np.random.default_rng(5)
+    noise = rng.integers(0, 4, (F, T), dtype=np.uint8)
+    vs = ViterbiStream(CODE, streams=F, soft=False, window_steps=96)
+    x = torch.from_numpy(noise).cuda()
+    got, counts = push_frame(vs, x, 1, [48] * (T // 48) + [T % 48])
+    lost = (counts == -1).any(axis=0)
+    assert lost.any()
+    want = expect_bits(orc, noise, L, False)
+    for f in range(F):
+        if lost[f]:
+            first = int(np.argmax(counts[:, f] == -1))
+            assert (counts[first:, f] == -1).all()
+        else:
+            assert (got[f] == want[f]).all(), f
+    # a clean frame afterwards
+    unc, xh = random_frames(orc, K, L, F, 0.0, 6)
+    got, counts = push_frame(vs, torch.from_numpy(xh).cuda(), 1, [48] * (T // 48) + [T % 48])
+    assert (counts >= 0).all()
+    want = np.unpackbits(unc, axis=1)[:, :L]
+    for f in range(F):
+        assert (got[f] == want[f]).all(), f
+
+
+def test_stream_api_errors():
+    import ctypes
+
+    L = native.lib()
+    c = CODE._c()
+    h = ctypes.c_void_p()
+    k9 = ConvCode(9, CODES[9])._c()
+    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(k9), 0, 4, 0, 0) == native.VTB_ERR_UNSUPPORTED
+    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(c), 0, 0, 0, 0) == native.VTB_ERR_INVALID
+    vs = ViterbiStream(CODE, streams=2, window_steps=96)
+    x = torch.zeros((2, 100), dtype=torch.uint8, device="cuda")
+    with pytest.raises(native.VtbError):
+        vs.push(x)  # more than window_steps - 48 segments in one call
+    with pytest.raises(native.VtbError):
+        vs.push(x[:, :3], last=True)  # a frame needs at least K segments

@@ -25,7 +25,13 @@ for s in $steps; do
     pmc)
       rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
-      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $? ;;
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $?
+      # VALU issue: wave-instructions per launch and the effective clock (GRBM_GUI_ACTIVE)
+      rm -rf gpurun_out/pmc_valu
+      timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_valu.log 2>&1 || exit $? ;;
+    isa)
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/isa_bench tools/probes/isa_bench.hip &&
+      timeout -k 10 120 /tmp/isa_bench > gpurun_out/isa_bench.log 2>&1 || exit $? ;;
   esac
 done
 exit 0

@@ -45,3 +45,25 @@ if os.path.exists(path):
 data[key] = round(total)
 json.dump(data, open(path, "w"), indent=1, sort_keys=True)
 print(key, "fetch KiB", fetch_kib, "write KiB", write_kib, "bytes/launch", total)
+
+# VALU issue pass (tools/gpu_check.sh pmc, third run): wave-level VALU instructions per launch,
+# for bench.py's roofline.secondary.  SQ counters are summed over the XCDs by rocprofv3;
+# GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back).
+if os.path.exists(os.path.join(root, "pmc_valu", "run_counter_collection.csv")):
+    names = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+             "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE")
+    v = {n: mean_counter("pmc_valu", n)[0] for n in names}
+    kt = os.path.join(root, "pmc_valu", "run_kernel_trace.csv")
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(kt))
+            if "kernel" in r["Kernel_Name"]]
+    dur_ns = sum(durs) / len(durs)
+    v["kernel_ns_profiled"] = dur_ns
+    v["effective_clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8.0 / dur_ns
+    with open(os.path.join(repo, "profiles", rnd, "pmc_valu_detail.json"), "w") as fh:
+        json.dump({"workload": key, **v}, fh, indent=1)
+    vpath = os.path.join(repo, "profiles", "pmc_valu.json")
+    vd = json.load(open(vpath)) if os.path.exists(vpath) else {}
+    # (effective_clock_ghz reads high on dispatches shorter than ~0.3 ms: kept in the detail file only)
+    vd[key] = {"valu_wave_insts_per_launch": round(v["SQ_INSTS_VALU"]), "waves_per_launch": round(v["SQ_WAVES"])}
+    json.dump(vd, open(vpath, "w"), indent=1, sort_keys=True)
+    print(key, "VALU insts/launch", v["SQ_INSTS_VALU"], "waves", v["SQ_WAVES"], "clock GHz", v["effective_clock_ghz"])
