@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--stream-chunk", type=int, default=0,
+                    help="measure the streaming decoder (vtb_stream_*, SURVEY.md 8 f3) instead: every stream "
+                         "receives this many segments per step, one long frame per stream")
     ap.add_argument("--gen", choices=("host", "device"), default="host",
                     help="synthetic frames from numpy on the host (default) or from the device generator "
                          "(csrc/vtb_gen.hip: no PCIe, for large batches)")
@@ -155,6 +158,56 @@ def load_valu(workload_key):
 VALU_PEAK_G = 256 * 4 * 2.4 / 4
 
 
+def stream_bench(args, dev, local, world):
+    """Steady-state streaming decode: F streams, one long frame each, C segments per stream
+    per step (a step = one vtb_stream_decode call, inputs already in HBM); value = segments
+    pushed per second (= decoded bits per second in steady state: the emitted bits trail
+    the input by the merge depth)."""
+    import torch
+
+    from convolutionalencdec_amd import ConvCode, ViterbiStream
+    from convolutionalencdec_amd import frames as devframes
+
+    F, C, soft = args.frames, args.stream_chunk, not args.hard
+    steps, warm = args.steps, args.warmup
+    L = (steps + warm) * C
+    d_unc, d_rx = devframes.make_frames(ConvCode(*(K, G)), F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
+                                        seed=shard_seed(int(os.environ.get("RANK", "0"))), device=local)
+    sb = 2 if soft else 1
+    x = d_rx.reshape(F, -1)
+    vs = ViterbiStream(ConvCode(K, G), streams=F, soft=soft, window_steps=max(4 * C, 4096), device=local)
+    outs = []
+
+    def push(i, last=False):
+        hi = x.shape[1] if last else (i + 1) * C * sb
+        o, nb = vs.push(x[:, i * C * sb:hi], last=last)
+        outs.append((o, nb))
+
+    for i in range(warm):
+        push(i)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(warm, warm + steps):
+        push(i)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    push(warm + steps, last=True)  # the tail, untimed
+    torch.cuda.synchronize(dev)
+    bits = np.concatenate([np.concatenate([np.unpackbits(o[f].cpu().numpy())[:int(nb[f])]
+                                           for o, nb in outs]) for f in range(min(F, 8))]).reshape(min(F, 8), -1)
+    unc = np.unpackbits(d_unc[:min(F, 8)].cpu().numpy(), axis=1)[:, :L]
+    ber = float((bits[:, :L] != unc).mean()) if bits.shape[1] == L else None
+    value = F * C * steps / dt / 1e6
+    line = {"metric": METRIC, "value": round(value, 2), "unit": "Mbit/s", "n_gpus": 1, "steps": steps, "warmup": warm,
+            "ms_per_step": round(dt / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u16", "data": "synthetic (device generator)",
+            "config": {"workload": f"streaming K=7 r=1/2 {'8-bit soft' if soft else 'hard'}-decision, {F} streams x "
+                                   f"{C} segments per call (vtb_stream_decode), one {L}-bit frame per stream",
+                       "streams": F, "segments_per_call": C, "decoded_ber_first8": ber},
+            "roofline": None, "cpu_baseline": None}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     world, rank, local = dist_env()
@@ -164,6 +217,10 @@ def main():
         raise SystemExit("bench.py needs a ROCm GPU")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.stream_chunk > 0:
+        if world > 1:
+            raise SystemExit("--stream-chunk is a single-GPU measurement")
+        return stream_bench(args, dev, local, world)
     if world > 1:
         import torch.distributed as dist
 

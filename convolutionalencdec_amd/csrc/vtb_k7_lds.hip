@@ -275,101 +275,141 @@ __device__ __forceinline__ void put_bits48_global(uint8_t* o, uint64_t bits) {
     o[4] = uint8_t(rh >> 24), o[5] = uint8_t(rh >> 16);
 }
 
-// Traceback of one streaming call (vtb_stream_decode).  Frame f of the wave has emitted the
-// decoded bits of steps [0, e_f) before the call.
-//  * Not last: walks from all 64 locations at t_end go back 48 steps at a time until they
-//    stand on one location (step m).  Every survivor path then passes through it, so no
-//    later input can change the path below m: the bits of [e_f, m) are final -- equal to
-//    the whole-frame decode's, hence the reference's -- and are emitted.  m <= t_end - 48,
-//    so the zero tail (the last K - 1 steps of a frame) is never emitted early.
+// Two survivor walks of 48 steps each over the global survivor words (the location part of
+// tb_body / tb_body8 only), their loads issued together: the merge test's walks are
+// latency-bound chains of dependent loads, so each lane carries two.
+template <bool SOFT>
+__device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint32_t& l4b, uint64_t gbase) {
+    uint32_t a = cb | l4a, b = cb | l4b;
+    if constexpr (SOFT) {
+#pragma unroll
+        for (int j = 0; j < 24; j++) {
+            const int todd = 47 - 2 * j;
+            const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+            uint32_t va, vb;
+            asm volatile("global_load_ushort %0, %2, %4 offset:%5\n\tglobal_load_ushort %1, %3, %4 offset:%5\n\t"
+                         "s_waitcnt vmcnt(0)"
+                         : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"((todd >> 4) * 256));
+            const int pos = 2 + (todd - 1) % 6;
+            const uint32_t fa = pos >= sh ? (va << (pos - sh)) : (va >> (sh - pos));
+            const uint32_t fb = pos >= sh ? (vb << (pos - sh)) : (vb >> (sh - pos));
+            a = (a & ~(3u << pos)) | (fa & (3u << pos));
+            b = (b & ~(3u << pos)) | (fb & (3u << pos));
+        }
+    } else {
+#pragma unroll
+        for (int k = 5; k >= 0; k--) {
+            const int r0 = (8 * k) % 6;
+            uint32_t va, vb;
+            asm volatile("global_load_ubyte %0, %2, %4 offset:%5\n\tglobal_load_ubyte %1, %3, %4 offset:%5\n\t"
+                         "s_waitcnt vmcnt(0)"
+                         : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"(256 * (k >> 1) + (k & 1)));
+            a = (a & ~0xFCu) | (rotl6c(va & 63u, r0) << 2);
+            b = (b & ~0xFCu) | (rotl6c(vb & 63u, r0) << 2);
+        }
+    }
+    l4a = a & 0xFCu;
+    l4b = b & 0xFCu;
+}
+
+// Traceback of one streaming call (vtb_stream_decode).  Frame f of the wave (lanes 32f ..
+// 32f + 31) has emitted the decoded bits of steps [0, e_f) before the call.
+//  * Not last: walks from all 64 locations at t_end (two per lane) go back 48 steps at a
+//    time until they stand on one location (step m).  Every survivor path then passes
+//    through it, so no later input can change the path below m: the bits of [e_f, m) are
+//    final -- equal to the whole-frame decode's, hence the reference's -- and are emitted.
+//    m <= t_end - 48, so the zero tail (the last K - 1 steps of a frame) is never emitted
+//    early.
 //  * Last: the terminated traceback from location 0 at T (the padding rows keep location 0,
 //    as in the frame decoder) emits [e_f, T - 6).
-// The emission is the frame decoder's verified block-parallel traceback over [e_f, hi) with
-// all 64 lanes on one frame, entering at the location known at hi.  If the ring no longer
-// holds step e_f (no merge within sa.ring steps) the frame is flagged: -1 bits until last.
+// The emission is the frame decoder's verified block-parallel traceback over [e_f, hi_f),
+// 32 blocks per frame, entering at the location known at hi_f.  If the ring no longer holds
+// step e_f (no merge within sa.ring steps) the frame is flagged: -1 bits until last.
 template <bool SOFT>
 __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
                                  uint64_t gbase, size_t fa, bool has_b) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
     uint32_t* st = sa.state + size_t(blockIdx.x) * kStreamStateWords;
-    int e[2] = {int(__builtin_amdgcn_readfirstlane(st[64])), int(__builtin_amdgcn_readfirstlane(st[65]))};
-    uint32_t flags = __builtin_amdgcn_readfirstlane(st[66]);
-    auto tb48 = [&](int tlo, int f, uint32_t& l4) -> uint64_t {
-        const uint32_t cb = uint32_t(2 * f + 256 * ((tlo % sa.ring) >> 4));
-        if constexpr (SOFT) return tb_body<true>(cb, l4, gbase);
-        else return tb_body8<true>(cb, l4, gbase);
+    const int e0 = int(st[64 + f]);  // this lane's frame
+    const uint32_t flags0 = __builtin_amdgcn_readfirstlane(st[66]);
+    const bool real = f == 0 || has_b;
+    const bool lost = ((flags0 >> f) & 1u) || t_end - e0 > sa.ring;
+    auto colb = [&](int tlo) { return uint32_t(2 * f + 256 * ((tlo % sa.ring) >> 4)); };
+    auto tb48 = [&](int tlo, uint32_t& l4) -> uint64_t {
+        if constexpr (SOFT) return tb_body<true>(colb(tlo), l4, gbase);
+        else return tb_body8<true>(colb(tlo), l4, gbase);
     };
-    for (int f = 0; f < 2; f++) {
-        if (f == 1 && !has_b) break;
-        const int e0 = e[f];
-        int bits_out;
-        if (((flags >> f) & 1u) || t_end - e0 > sa.ring) {
-            flags |= 1u << f;
-            bits_out = -1;
-        } else {
-            int hi = e0, kfrom = e0;
-            uint32_t kloc = 0;
-            if (sa.last) {
-                hi = t_end, kfrom = T;
-            } else {
-                uint32_t l4 = 4u * uint32_t(lane);  // every location (l' = lane)
-                for (int tlo = t_end - 48; tlo >= e0; tlo -= 48) {
-                    (void)tb48(tlo, f, l4);
-                    const uint32_t l0 = __builtin_amdgcn_readfirstlane(l4);
-                    if (__all(l4 == l0)) {
-                        hi = kfrom = tlo, kloc = l0;
-                        break;
-                    }
-                }
+
+    int hi = e0, kfrom = e0;
+    uint32_t kloc = 0;
+    if (sa.last) {
+        hi = t_end, kfrom = T;
+    } else {
+        // merge test: lane j of frame f walks locations l' = j and j + 32
+        uint32_t la = 4u * uint32_t(blk), lb = la + 128u;
+        bool walking = !lost && real;
+        for (int tlo = t_end - 48; __builtin_amdgcn_readfirstlane(__ballot(walking && tlo >= e0) != 0); tlo -= 48) {
+            const bool here = walking && tlo >= e0;
+            if (here) tb_walk48_pair<SOFT>(colb(tlo), la, lb, gbase);
+            const uint32_t ref = __shfl(la, 32 * f);
+            const uint64_t same = __ballot(la == ref && lb == ref);
+            const bool merged = uint32_t(same >> (32 * f)) == 0xFFFFFFFFu;
+            if (here && merged) {
+                hi = kfrom = tlo, kloc = ref;
+                walking = false;
             }
-            if (hi > e0) {
-                const int n = hi - e0;                              // multiple of 48
-                const int tbb = ((n + 63) / 64 + 47) / 48 * 48;     // 64 blocks of whole sextet-octets
-                const int bot = e0 + lane * tbb;
-                const bool active = bot < hi;
-                const int start_full = bot + tbb + kTbWarm;
-                const int start = min(start_full, hi);
-                const bool known = start >= kfrom;
-                const int nbody = (kTbWarm + tbb) / 48;
-                uint8_t* ob = out + (fa + f) * out_stride;  // byte (tlo - e0) / 8 of the call's bits
-                uint32_t loc = known ? kloc : 0u, loc_top = loc;
-                if (active) {
-                    for (int g = 0; g < nbody; g++) {
-                        const int tlo = start_full - 48 * (g + 1);
-                        if (g == kTbWarm / 48) loc_top = loc;
-                        if (tlo < start) {
-                            const uint64_t bits = tb48(tlo, f, loc);
-                            if (g >= kTbWarm / 48) put_bits48_global(ob + ((tlo - e0) >> 3), bits);
-                        }
-                    }
-                }
-                // verification, as in the frame decoder (one frame over 64 blocks)
-                uint32_t fin = loc;
-                bool fixed = known || !active;
-                for (int round = 0; round < 65; round++) {
-                    const uint32_t sf = __shfl_down(fin, 1);
-                    const bool ok = fixed || loc_top == sf;
-                    const uint64_t bad = ~__ballot(ok);
-                    if (bad == 0) break;
-                    const bool succ_proven = lane == 63 || (bad >> (lane + 1)) == 0;
-                    if (!ok && succ_proven) {
-                        loc = sf;
-                        for (int g = kTbWarm / 48; g < nbody; g++) {
-                            const int tlo = start_full - 48 * (g + 1);
-                            put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, f, loc));
-                        }
-                        fin = loc;
-                        fixed = true;
-                    }
-                }
-            }
-            bits_out = sa.last ? T - 6 - e0 : hi - e0;
-            e[f] = hi;
+            if (tlo < e0) walking = false;
         }
-        if (lane == 0) sa.out_bits[fa + f] = bits_out;
     }
-    if (sa.last) e[0] = e[1] = 0, flags = 0;  // the streams restart with the next frame
-    if (lane == 0) st[64] = uint32_t(e[0]), st[65] = uint32_t(e[1]), st[66] = flags;
+    if (!lost && real && hi > e0) {
+        const int n = hi - e0;                           // multiple of 48
+        const int tbb = ((n + 31) / 32 + 47) / 48 * 48;  // 32 blocks per frame
+        const int bot = e0 + blk * tbb;
+        const bool active = bot < hi;
+        const int start_full = bot + tbb + kTbWarm;
+        const int start = min(start_full, hi);
+        const bool known = start >= kfrom;
+        const int nbody = (kTbWarm + tbb) / 48;
+        uint8_t* ob = out + (fa + f) * out_stride;  // byte (tlo - e0) / 8 of the call's bits
+        uint32_t loc = known ? kloc : 0u, loc_top = loc;
+        if (active) {
+            for (int g = 0; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                if (g == kTbWarm / 48) loc_top = loc;
+                if (tlo < start) {
+                    const uint64_t bits = tb48(tlo, loc);
+                    if (g >= kTbWarm / 48) put_bits48_global(ob + ((tlo - e0) >> 3), bits);
+                }
+            }
+        }
+        // verification, as in the frame decoder (the last active block of a frame is known)
+        uint32_t fin = loc;
+        bool fixed = known || !active;
+        for (int round = 0; round < 33; round++) {
+            const uint32_t sf = __shfl_down(fin, 1);
+            const bool ok = fixed || loc_top == sf;
+            const uint64_t bad = ~__ballot(ok);
+            const uint32_t badf = uint32_t(bad >> (32 * f));
+            if (badf == 0) break;
+            const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+            if (!ok && succ_proven) {
+                loc = sf;
+                for (int g = kTbWarm / 48; g < nbody; g++) {
+                    const int tlo = start_full - 48 * (g + 1);
+                    put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, loc));
+                }
+                fin = loc;
+                fixed = true;
+            }
+        }
+    }
+    const int bits_out = lost ? -1 : sa.last ? T - 6 - e0 : hi - e0;
+    if (real && blk == 0) sa.out_bits[fa + f] = bits_out;
+    // new emission state; the streams restart after last
+    const uint64_t lostmask = __ballot(lost && real && blk == 0);
+    const uint32_t flags = sa.last ? 0u : uint32_t((lostmask & 1u) | ((lostmask >> 32) & 1u) << 1);
+    if (blk == 0) st[64 + f] = uint32_t(sa.last || lost ? (sa.last ? 0 : e0) : hi);
+    if (lane == 0) st[66] = flags;
 }
 
 // GS = false: survivor words in LDS at [r0, r0 + 16 Tpad).  GS = true: survivor words in a
