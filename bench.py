@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: step i runs on stream i mod inflight (own plan and output), so one "
+                         "batch's tail overlaps the next one's start")
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="measure the streaming decoder (vtb_stream_*, SURVEY.md 8 f3) instead: every stream "
                          "receives this many segments per step, one long frame per stream")
@@ -258,21 +261,32 @@ def main():
         unc, rx = synth.make_frames(code[0], code[1], F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
                                     seed=shard_seed(rank))
         x = torch.from_numpy(rx.reshape(F, -1)).to(dev)
-    dec = ViterbiDecoder(ConvCode(*code), frame_bits=L, soft=soft, device=local)
-    out = torch.empty((F, (L + 7) // 8), dtype=torch.uint8, device=dev)
+    nin = max(1, args.inflight)
+    decs = [ViterbiDecoder(ConvCode(*code), frame_bits=L, soft=soft, device=local) for _ in range(nin)]
+    outs = [torch.empty((F, (L + 7) // 8), dtype=torch.uint8, device=dev) for _ in range(nin)]
     stream = torch.cuda.current_stream(dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nin - 1)]
+    dec, out = decs[0], outs[0]
+    state = {"i": 0}
 
     def step():
-        dec.decode_device(x, out=out, stream=stream.cuda_stream)
+        i = state["i"] % nin
+        state["i"] += 1
+        decs[i].decode_device(x, out=outs[i], stream=streams[i].cuda_stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]) or args.warmup < nin
     decoded = out.cpu().numpy()
     ber = float(np.unpackbits(decoded ^ unc).mean())
 
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
     elapsed = timer.run(step, args.steps)
+
+    def step():  # noqa: F811 -- single-stream launches for the per-launch duration below
+        dec.decode_device(x, out=out, stream=stream.cuda_stream)
 
     # Average launch duration with HIP events on the launch stream (roofline numerator): one
     # event pair around K back-to-back launches, as rocprofv3's per-kernel average sees them.
@@ -329,6 +343,7 @@ def main():
             "frame_bits": L,
             "global_batch_frames": F * world,
             "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
+            "batches_in_flight": nin,
             "decoded_ber": ber,
         },
         "roofline": {

@@ -120,6 +120,12 @@ __host__ __device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ ((
 // result (one wait state each way: tools/probes/permlane_hazard.hip).
 template <int P>
 __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, uint32_t& B) {
+#ifdef VTB_EXP_NONOP
+    // measurement only (wrong results): A and B without the hazard wait states, to bound
+    // what filling them could gain (the min is fused in by step_nonop below)
+    A = m, B = vw.x ^ vw.y;
+    return;
+#endif
     if constexpr (P == 4 || P == 5) {
         if constexpr (P == 4) {
             asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
@@ -142,7 +148,13 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
 // One v_bfi_b32 (the compiler otherwise splits a constant-mask select into and/and/or).
 __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b) {
     uint32_t r;
+#ifdef VTB_EXP_BITOP3
+    // v_bitop3_b32 with the bit-select truth table: issues at the fast (two-pass) rate,
+    // v_bfi_b32 at the four-cycle rate (profiles/r01/isa_bench*.txt)
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+#else
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+#endif
     return r;
 }
 
@@ -252,6 +264,32 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
 #define VTB_EXP_WORD(x) asm volatile("" ::"v"(z))
 #else
 #define VTB_EXP_WORD(x) x
+#endif
+
+#ifdef VTB_EXP_NONOP
+#define VTB_EXP_ACS(P, M, vw) M = step_nonop<P>(M, vw);
+#else
+#define VTB_EXP_ACS(P, M, vw)                                                                    \
+    {                                                                                            \
+        uint32_t A, B;                                                                           \
+        candidates<P>(M, vw, A, B);                                                              \
+        M = pk_min(A, B);                                                                        \
+    }
+#endif
+#ifdef VTB_EXP_NONOP
+template <int P>
+__device__ __forceinline__ uint32_t step_nonop(uint32_t m, uint2 vw) {
+    uint32_t A, B;
+#define VTB_NN(X) asm volatile("v_add_u32 %1, %0, %3\n\t" X "\n\tv_pk_min_u16 %0, %1, %2" : "+v"(m), "=&v"(A), "=&v"(B) : "v"(vw.x), "v"(vw.y));
+    if constexpr (P == 5) VTB_NN("v_permlane32_swap_b32 %0, %0\n\tv_add_u32 %2, %0, %4")
+    if constexpr (P == 4) VTB_NN("v_permlane16_swap_b32 %0, %0\n\tv_add_u32 %2, %0, %4")
+    if constexpr (P == 3) VTB_NN("v_add_u32_dpp %2, %0, %4 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    if constexpr (P == 2) VTB_NN("v_add_u32_dpp %2, %0, %4 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    if constexpr (P == 1) VTB_NN("v_add_u32_dpp %2, %0, %4 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    if constexpr (P == 0) VTB_NN("v_add_u32_dpp %2, %0, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1")
+#undef VTB_NN
+    return m;
+}
 #endif
 
 // Survivor word W (of the chunk's three) of this lane: LDS store, or a global store at
@@ -585,9 +623,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             const uint32_t ref = __builtin_amdgcn_readfirstlane(M);                              \
             asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(H::BIAS * kR1), "s"(ref) : "scc");       \
         }                                                                                        \
-        uint32_t A, B;                                                                           \
-        candidates<5 - (PH)>(M, VTB_EXP_VW(cur[PH], I), A, B);                                   \
-        M = pk_min(A, B);                                                                        \
+        VTB_EXP_ACS(5 - (PH), M, VTB_EXP_VW(cur[PH], I))                                         \
         if (SOFT && ((I) & 1)) {                                                                 \
             /* window (I) >> 1 & 7 of the word: history bytes of two windows by one v_perm */    \
             const int w = ((I) & 15) >> 1;                                                       \
@@ -627,8 +663,19 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_STEP(6 * (G) + 2, 2) VTB_STEP(6 * (G) + 3, 3)                                         \
         VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                                         \
     }
+#if !defined(VTB_EXP_RD1) && !defined(VTB_EXP_NO_TABREAD) && !defined(VTB_EXP_TAB32) && VTB_EXP_AHEAD == 2
+// Even groups read the next two groups' pairs of one phase (rows 6 apart in one column of
+// the ring): one ds_read2_b64 per phase and group pair, half the LDS read instructions of
+// one ds_read_b64 per step (measured 2% faster).  (VTB_EXP_RD1: one read per step.)
+#define VTB_RD(G, k)                                                                              \
+    if (((G) & 1) == 0) {                                                                         \
+        buf[((G) + 2) & 3][k] = ap[k][(6 * ((G) + 2) + (k)) % kChunk];                            \
+        buf[((G) + 3) & 3][k] = ap[k][(6 * ((G) + 3) + (k)) % kChunk];                            \
+    }
+#else
 #define VTB_RD(G, k)                                                                              \
     buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk], buf[(G) & 3][k]);
+#endif
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP

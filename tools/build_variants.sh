@@ -24,6 +24,9 @@ for v in "$@"; do
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
     base) build base ;;
+    nonop) build nonop -DVTB_EXP_NONOP ;;
+    bitop3) build bitop3 -DVTB_EXP_BITOP3 ;;
+    rd1) build rd1 -DVTB_EXP_RD1 ;;
     tab32) build tab32 -DVTB_EXP_TAB32 ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;

@@ -21,14 +21,23 @@ for s in $steps; do
       timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 0 --frames 65536 > gpurun_out/bench_65k.log 2>&1 || exit $? ;;
     prof)
       rm -rf gpurun_out/prof
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 > gpurun_out/prof.log 2>&1 || exit $? ;;
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 > gpurun_out/prof.log 2>&1 || exit $?
+      rm -rf gpurun_out/prof_hard
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_hard -o run -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --hard > gpurun_out/prof_hard.log 2>&1 || exit $? ;;
     pmc)
-      rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
-      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
-      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_write.log 2>&1 || exit $?
-      # VALU issue: wave-instructions per launch and the effective clock (GRBM_GUI_ACTIVE)
-      rm -rf gpurun_out/pmc_valu
-      timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/pmc_valu.log 2>&1 || exit $? ;;
+      # per workload: FETCH_SIZE, WRITE_SIZE and the SQ VALU pass, each its own rocprofv3 run
+      for wl in soft hard; do
+        args="--steps 20 --warmup 2 --cpu-seconds 0"; [ $wl = hard ] && args="$args --hard"
+        for pass in fetch write valu; do
+          case $pass in
+            fetch) ctr="FETCH_SIZE" ;;
+            write) ctr="WRITE_SIZE" ;;
+            valu) ctr="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" ;;
+          esac
+          rm -rf gpurun_out/pmc_${wl}/pmc_$pass
+          timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d gpurun_out/pmc_${wl}/pmc_$pass -o run -- python3 bench.py $args > gpurun_out/pmc_${wl}_$pass.log 2>&1 || exit $?
+        done
+      done ;;
     isa)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/isa_bench tools/probes/isa_bench.hip &&
       timeout -k 10 120 /tmp/isa_bench > gpurun_out/isa_bench.log 2>&1 || exit $? ;;

@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"  # holds pmc_fetch/, pmc_write/, pmc_valu/
 rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
 key = sys.argv[3] if len(sys.argv) > 3 else "K7_soft_F4096_L1024"
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,10 +31,11 @@ def mean_counter(d, name):
 
 fetch_kib, nf = mean_counter("pmc_fetch", "FETCH_SIZE")
 write_kib, nw = mean_counter("pmc_write", "WRITE_SIZE")
+tag = key.split("_")[1]  # soft / hard: detail files per workload
 FETCH_CORRECTION = 2.0
 total = (FETCH_CORRECTION * fetch_kib + write_kib) * 1024.0
 os.makedirs(os.path.join(repo, "profiles", rnd), exist_ok=True)
-with open(os.path.join(repo, "profiles", rnd, "pmc_traffic_detail.json"), "w") as fh:
+with open(os.path.join(repo, "profiles", rnd, f"pmc_traffic_detail_{tag}.json"), "w") as fh:
     json.dump({"workload": key, "fetch_kib_per_dispatch_raw": fetch_kib, "fetch_correction": FETCH_CORRECTION,
                "write_kib_per_dispatch": write_kib,
                "dispatches": [nf, nw], "bytes_per_launch": total}, fh, indent=1)
@@ -59,7 +60,7 @@ if os.path.exists(os.path.join(root, "pmc_valu", "run_counter_collection.csv")):
     dur_ns = sum(durs) / len(durs)
     v["kernel_ns_profiled"] = dur_ns
     v["effective_clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8.0 / dur_ns
-    with open(os.path.join(repo, "profiles", rnd, "pmc_valu_detail.json"), "w") as fh:
+    with open(os.path.join(repo, "profiles", rnd, f"pmc_valu_detail_{tag}.json"), "w") as fh:
         json.dump({"workload": key, **v}, fh, indent=1)
     vpath = os.path.join(repo, "profiles", "pmc_valu.json")
     vd = json.load(open(vpath)) if os.path.exists(vpath) else {}
