@@ -77,12 +77,16 @@ class Timer:
     def __init__(self, world, device_sync, barrier, allreduce_max):
         self.world, self.sync, self.barrier, self.allreduce_max = world, device_sync, barrier, allreduce_max
 
-    def run(self, step, steps):
+    def run(self, step, steps, on_start=None, on_end=None):
         self.barrier()
         self.sync()
         t0 = time.perf_counter()
+        if on_start:
+            on_start()  # e.g. a HIP event on the launch stream (asynchronous, enqueue only)
         for _ in range(steps):
             step()
+        if on_end:
+            on_end()
         self.sync()
         dt = time.perf_counter() - t0  # this rank's K steps; the closing barrier is not timed
         self.barrier()
@@ -282,21 +286,36 @@ def main():
     decoded = out.cpu().numpy()
     ber = float(np.unpackbits(decoded ^ unc).mean())
 
+    # Average launch duration for the roofline: HIP events on the launch stream around the
+    # timed region's K back-to-back launches (what rocprofv3's per-kernel average sees).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
-    elapsed = timer.run(step, args.steps)
+    elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
-    def step():  # noqa: F811 -- single-stream launches for the per-launch duration below
+    def step():  # noqa: F811 -- single-stream launches (per-launch duration with --inflight > 1)
         dec.decode_device(x, out=out, stream=stream.cuda_stream)
 
-    # Average launch duration with HIP events on the launch stream (roofline numerator): one
-    # event pair around K back-to-back launches, as rocprofv3's per-kernel average sees them.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if nin > 1:
+        # the timed region interleaves streams: time K launches on one stream instead
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        kern_ms = ev0.elapsed_time(ev1) / args.steps
+
+    # PCIe-inclusive rate: the same batch from pageable host memory through
+    # vtb_decode_host (H2D copy, decode, D2H copy, synchronise); reported beside, never `value`.
+    host_mbps = None
+    if args.gen == "host" and world == 1:
+        rx_host = np.ascontiguousarray(rx.reshape(F, -1))
+        dec.decode_host(rx_host)
+        reps = 10
+        th = time.perf_counter()
+        for _ in range(reps):
+            dec.decode_host(rx_host)
+        host_mbps = round(F * L * reps / (time.perf_counter() - th) / 1e6, 1)
 
     ms_per_step = elapsed / args.steps * 1e3
     total_bits = F * L * world
@@ -344,6 +363,7 @@ def main():
             "global_batch_frames": F * world,
             "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
             "batches_in_flight": nin,
+            "host_buffers_mbps": host_mbps,
             "decoded_ber": ber,
         },
         "roofline": {

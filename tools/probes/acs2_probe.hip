@@ -1,0 +1,150 @@
+// Probe: the K=7 ACS step with two metric registers per lane (32 lanes per frame pair, four
+// frames per wave64) against the shipped layout (one register per lane, 64 lanes per frame
+// pair).  With two registers, one of the six location bits is the register index (the
+// butterfly runs inside the lane with plain adds) and XOR 32 disappears; the XOR-16 phase
+// exchanges rows between the two registers with one v_permlane16_swap (a transposition:
+// afterwards each lane holds a partner pair) and then also runs inside the lane.  Bits 5
+// and 4 take turns as the register bit, so each six-step period has two transpositions.
+// Table values live in registers (no LDS), so this isolates VALU/DPP/permlane issue.
+// Prints cycles per frame-pair-step per SIMD at the nominal clock.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t m, uint32_t w) {
+    return __builtin_amdgcn_update_dpp(0u, m, CTRL, 0xF, 0xF, true) + w;
+}
+
+// In-lane butterfly of a partner pair (r0, r1): 4 plain adds, 2 mins.
+__device__ __forceinline__ void inlane(uint32_t& r0, uint32_t& r1, uint4 t) {
+    const uint32_t a0 = r0 + t.x, b0 = r1 + t.y, a1 = r1 + t.z, b1 = r0 + t.w;
+    r0 = pk_min(a0, b0);
+    r1 = pk_min(a1, b1);
+}
+template <int CTRL>
+__device__ __forceinline__ void dppstep(uint32_t& r, uint2 t) {
+    r = pk_min(r + t.x, dpp_add<CTRL>(r, t.y));
+}
+
+// Two registers per lane: 6 steps = reg phase, x16 phase, 4 DPP phases (x8, x7, x2, x1).
+__global__ __launch_bounds__(64) void k2(uint64_t* out, int iters, uint32_t seed) {
+    const int lane = threadIdx.x;
+    uint32_t r0 = 8192u * 0x10001u + lane, r1 = r0 + 3;
+    uint4 tq[2];
+    uint2 td[4][2];
+    for (int i = 0; i < 2; i++) tq[i] = make_uint4(seed * (i + 1) + lane, seed ^ lane, seed + 7 * lane, lane * 13);
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 2; j++) td[i][j] = make_uint2((seed * (i + 3) + lane + j) & 0x01ff01ffu, (seed ^ (lane * 77 + i + j)) & 0x01ff01ffu);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            // bits 5 and 4 alternate between the register and the lane row: a transposition
+            // before each of the two in-lane steps
+            asm volatile("s_nop 0\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 0" : "+v"(r0), "+v"(r1));
+            inlane(r0, r1, tq[0]);
+            asm volatile("s_nop 0\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 0" : "+v"(r0), "+v"(r1));
+            inlane(r0, r1, tq[1]);
+            r0 &= 0xFFFCFFFCu, r1 &= 0xFFFCFFFCu;
+            dppstep<0x128>(r0, td[0][0]), dppstep<0x128>(r1, td[0][1]);
+            dppstep<0x141>(r0, td[1][0]), dppstep<0x141>(r1, td[1][1]);
+            r0 &= 0xFFFCFFFCu, r1 &= 0xFFFCFFFCu;
+            dppstep<0x4E>(r0, td[2][0]), dppstep<0x4E>(r1, td[2][1]);
+            dppstep<0xB1>(r0, td[3][0]), dppstep<0xB1>(r1, td[3][1]);
+            r0 &= 0xFFFCFFFCu, r1 &= 0xFFFCFFFCu;
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x] = t1 - t0;
+    if ((r0 ^ r1) == 0x12345678u) out[1 << 20] = r0;
+}
+
+// Shipped layout, one register per lane: 6 steps = x32, x16 (in-place permlane swaps),
+// x8, x7, x2, x1 (DPP); C independent chains per wave.
+template <int C>
+__global__ __launch_bounds__(64) void k1(uint64_t* out, int iters, uint32_t seed) {
+    const int lane = threadIdx.x;
+    uint32_t M[C];
+    uint2 vw[6][C];
+    for (int c = 0; c < C; c++) {
+        M[c] = 8192u * 0x10001u + lane + c;
+        for (int i = 0; i < 6; i++)
+            vw[i][c] = make_uint2((seed * (i + 1) + lane + c) & 0x01ff01ffu, (seed ^ (lane * 77 + i + c)) & 0x01ff01ffu);
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                uint32_t A = M[c] + vw[0][c].x, m = M[c];
+                asm volatile("v_permlane32_swap_b32 %0, %0\n\ts_nop 0" : "+v"(m));
+                M[c] = pk_min(A, m + vw[0][c].y);
+            }
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                uint32_t A = M[c] + vw[1][c].x, m = M[c];
+                asm volatile("v_permlane16_swap_b32 %0, %0\n\ts_nop 0" : "+v"(m));
+                M[c] = pk_min(A, m + vw[1][c].y);
+                M[c] &= 0xFFFCFFFCu;
+            }
+#pragma unroll
+            for (int c = 0; c < C; c++) dppstep<0x128>(M[c], vw[2][c]);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                dppstep<0x141>(M[c], vw[3][c]);
+                M[c] &= 0xFFFCFFFCu;
+            }
+#pragma unroll
+            for (int c = 0; c < C; c++) dppstep<0x4E>(M[c], vw[4][c]);
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                dppstep<0xB1>(M[c], vw[5][c]);
+                M[c] &= 0xFFFCFFFCu;
+            }
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t x = 0;
+    for (int c = 0; c < C; c++) x ^= M[c];
+    if (lane == 0) out[blockIdx.x] = t1 - t0;
+    if (x == 0x12345678u) out[1 << 20] = x;
+}
+
+template <typename F>
+double run(F kern, int cus, int wps, int pairs_per_wave, double mhz) {
+    uint64_t* d;
+    (void)hipMalloc(&d, (size_t(1) << 20) * 8 + 8);
+    const int iters = 2000, steps = iters * 24;
+    const int blocks = cus * 4 * wps;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, 0, d, iters, 12345u);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, 0, d, iters, 12345u);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipFree(d);
+    return ms * 1e-3 * mhz * 1e6 / (double(steps) * pairs_per_wave * wps);
+}
+
+int main() {
+    hipDeviceProp_t p;
+    (void)hipGetDeviceProperties(&p, 0);
+    const double mhz = 2400.0;
+    const int cus = p.multiProcessorCount;
+    for (int wps : {1, 2, 4}) {
+        printf("W=%d waves/SIMD: shipped C=1 %.2f  shipped C=2 %.2f  two-register %.2f  cycles per frame-pair-step per SIMD\n",
+               wps, run(k1<1>, cus, wps, 1, mhz), run(k1<2>, cus, wps, 2, mhz), run(k2, cus, wps, 2, mhz));
+    }
+    return 0;
+}
