@@ -193,11 +193,16 @@ def stream_bench(args, dev, local, world):
     for i in range(warm):
         push(i)
     torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(warm, warm + steps):
         push(i)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    call_ms = ev0.elapsed_time(ev1) / steps
     push(warm + steps, last=True)  # the tail, untimed
     torch.cuda.synchronize(dev)
     bits = np.concatenate([np.concatenate([np.unpackbits(o[f].cpu().numpy())[:int(nb[f])]
@@ -205,13 +210,18 @@ def stream_bench(args, dev, local, world):
     unc = np.unpackbits(d_unc[:min(F, 8)].cpu().numpy(), axis=1)[:, :L]
     ber = float((bits[:, :L] != unc).mean()) if bits.shape[1] == L else None
     value = F * C * steps / dt / 1e6
+    alg = F * (C * sb + C // 8)  # input segments in, decoded bits out (steady state)
     line = {"metric": METRIC, "value": round(value, 2), "unit": "Mbit/s", "n_gpus": 1, "steps": steps, "warmup": warm,
             "ms_per_step": round(dt / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u16", "data": "synthetic (device generator)",
             "config": {"workload": f"streaming K=7 r=1/2 {'8-bit soft' if soft else 'hard'}-decision, {F} streams x "
                                    f"{C} segments per call (vtb_stream_decode), one {L}-bit frame per stream",
                        "streams": F, "segments_per_call": C, "decoded_ber_first8": ber},
-            "roofline": None, "cpu_baseline": None}
+            "roofline": {"bound": "hbm", "achieved": round(alg / (call_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6), "traffic": None,
+                         "kernel_ms": round(call_ms, 5), "algorithmic_bytes_per_launch": alg,
+                         "note": "one call = the stream kernel (+ a 2-D carry copy when C is not a multiple of 48)"},
+            "cpu_baseline": None}
     print(json.dumps(line), flush=True)
 
 

@@ -67,8 +67,18 @@ constexpr int kAH = 2;                   // table rows read this many steps ahea
 constexpr int kRS = 3;                   // register ring slots (48 % kRS == 0)
 constexpr int kTbWarm = 48;              // traceback warm-up steps past a block's end
 constexpr uint32_t kR1 = 0x10001u;
-constexpr uint32_t kHist = 0x00030003u;
 constexpr int kColBytes = 1024;          // survivor column: 256 words per 16 steps
+
+// History bits per u16 half (as vtb_k7_lds.hip): soft input keeps 4m + h (2 history bits);
+// hard input, whose metrics stay below 256, keeps 256m + h with 8 history
+// bits -- tie bit at t mod 8, survivor byte and clear every 8 steps, renormalisation once per
+// 48-step chunk, and an octet (8 steps, all of l') per traceback read.
+template <bool SOFT>
+struct Hist {
+    static constexpr int HB = SOFT ? 2 : 8;
+    static constexpr uint32_t SC = 1u << HB;
+    static constexpr uint32_t MASK = (SC - 1) * 0x10001u;
+};
 
 int tb_block(int Tq) {
     const int per = (Tq + 31) / 32;  // 32 blocks per frame, multiple of 48 steps
@@ -174,6 +184,25 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t 
     return bits;
 }
 
+// Hard input: 48 traceback steps as six octets, one byte read each.  The byte of octet k
+// (steps tlo + 8k + b) at the survivor's location holds the decisions D_b along its path, and
+// D_b is l' bit b (step t's pairing bit is bit t mod 8 of l'), so the location eight steps
+// back is the byte itself and the octet's eight decoded bits are its end location l'.
+__device__ __forceinline__ uint64_t tb_body8(uint32_t cb, uint32_t& la, uint64_t gbase) {
+    uint32_t a = cb | la;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int k = 5; k >= 0; k--) {
+        bits |= uint64_t(lprime_of(a)) << (8 * k);
+        uint32_t v;
+        asm volatile("global_load_ubyte %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                     : "=v"(v) : "v"(a), "s"(gbase), "i"(kColBytes * (k >> 1) + (k & 1)));
+        a = (a & ~0x3FCu) | (v & 0xFCu) | ((v & 3u) << 8);
+    }
+    la = a & 0x3FCu;
+    return bits;
+}
+
 __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) {
     unsigned short* o = reinterpret_cast<unsigned short*>(ob + (tlo >> 3));
     const uint32_t r = __builtin_bitreverse32(uint32_t(bits)), rh = __builtin_bitreverse32(uint32_t(bits >> 32));
@@ -188,7 +217,8 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
                                                 int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
                                                 uint8_t* __restrict__ ws, size_t ws_wave) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
-    constexpr uint32_t B4 = 4 * 16 * Q;  // renormalised metric of location 0, times four
+    using H = Hist<SOFT>;
+    constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
     extern __shared__ uint4 smem4[];
     uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
     const int lane = threadIdx.x;
@@ -232,11 +262,11 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
             q1 = (q0 >> 1) & kR1;
             q0 &= kR1;
         }
-        q0 <<= 2;
-        q1 <<= 2;
-        constexpr uint32_t QQ = 4 * Q * kR1;
+        q0 <<= H::HB;
+        q1 <<= H::HB;
+        constexpr uint32_t QQ = H::SC * Q * kR1;
         e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
-        const uint32_t tie = (1u + (srow & 1)) * kR1;
+        const uint32_t tie = (1u << (srow & (H::HB - 1))) * kR1;
 #pragma unroll
         for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
     };
@@ -250,9 +280,14 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
 #undef VTB_W2
-        if (c == 0 && srow < delta) {  // the own-keeping start step (odd T)
+        // Own-keeping rows: the start step of odd T; for hard input also the padding steps
+        // past Tq (W = the metric spread nQS + 1 keeps every survivor at its own location,
+        // so the octet that straddles Tq holds the true path's bits; for soft input that W
+        // would overflow u16, and the padding survivor bits are overwritten after the ACS).
+        const bool pad_row = !SOFT && (c + 1) * kCh > Tq && c * kCh + srow >= Tq;
+        if ((c == 0 && srow < delta) || pad_row) {
             uint2* col = reinterpret_cast<uint2*>(tab) + srow;
-            constexpr uint32_t PADW = 4 * (2 * Q + 1) * kR1;
+            constexpr uint32_t PADW = H::SC * ((SOFT ? 2 : 16) * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -263,8 +298,8 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     };
 
     uint32_t M[4];
-    M[0] = (lane == 0) ? B4 * kR1 : (B4 + 4 * Q) * kR1;
-    M[1] = M[2] = M[3] = (B4 + 4 * Q) * kR1;
+    M[0] = (lane == 0) ? B4 * kR1 : (B4 + H::SC * Q) * kR1;
+    M[1] = M[2] = M[3] = (B4 + H::SC * Q) * kR1;
     uint32_t ra, rb;
     {
         uint32_t e[4], et[4];
@@ -295,7 +330,10 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
                 stage_compute(ra, rb, se, set);
             }
             if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);  // all rows of this chunk read
-            if constexpr ((I % 12) == 10) {
+            // renormalisation reference: location 0 at a step whose history is clear
+            constexpr bool RN_READ = SOFT ? (I % 12) == 10 : I == 40;
+            constexpr bool RN_APPLY = SOFT ? (I % 12) == 11 : I == 47;
+            if constexpr (RN_READ) {
                 const uint32_t ref = __builtin_amdgcn_readfirstlane(M[0]);
                 asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(B4 * kR1), "s"(ref) : "scc");
             }
@@ -310,13 +348,29 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) M[r] = pk_min(A[r], Bc[r]);
-            if constexpr (I & 1) {
+            if constexpr (!SOFT && (I & 7) == 7) {
+                // octet history bytes: [A oct 0, A oct 1, B oct 0, B oct 1] per 16 steps
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    if constexpr ((I & 15) == 7) m_prev[r] = M[r];
+                    else pw[r][0] = __builtin_amdgcn_perm(M[r], m_prev[r], 0x06020400u);
+                    M[r] = RN_APPLY ? ((M[r] & ~H::MASK) + dd) : (M[r] & ~H::MASK);
+                }
+                if constexpr ((I & 15) == 15) {
+                    constexpr int W = I >> 4;
+                    gstore<W * kColBytes + 256 * rev2(0)>(gvo, pw[0][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(1)>(gvo, pw[1][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(2)>(gvo, pw[2][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(3)>(gvo, pw[3][0], gbase);
+                }
+            }
+            if constexpr (SOFT && (I & 1)) {
                 constexpr int w = (I & 15) >> 1;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     if constexpr (w & 1) pw[r][w >> 1] = __builtin_amdgcn_perm(M[r], m_prev[r], 0x06020400u);
                     else m_prev[r] = M[r];
-                    M[r] = ((I % 12) == 11) ? ((M[r] & ~kHist) + dd) : (M[r] & ~kHist);
+                    M[r] = RN_APPLY ? ((M[r] & ~H::MASK) + dd) : (M[r] & ~H::MASK);
                 }
                 if constexpr ((I & 15) == 15) {
                     constexpr int W = I >> 4;
@@ -337,9 +391,9 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // Padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping decisions
-    // (both history bits = the location's own bits t_even mod 8, +1 of l').
-    if (!(dbg & 2)) {
+    // Soft input, padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping
+    // decisions (both history bits = the location's own bits t_even mod 8, +1 of l').
+    if (SOFT && !(dbg & 2)) {
         uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + blockIdx.x * ws_wave);
         for (int g = Tq >> 4; g < (Tpad >> 4); g++) {
             const int w0 = Tq > 16 * g ? (Tq - 16 * g) >> 1 : 0;  // first padding window of the word
@@ -372,12 +426,16 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     const int start = min(start_full, Tpad);
     const bool known = start >= Tq;
     const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;
+    auto tb48 = [&](uint32_t cb, uint32_t& la) {
+        if constexpr (SOFT) return tb_body(cb, la, gbase);
+        else return tb_body8(cb, la, gbase);
+    };
     uint32_t loc = 0, loc_top = 0;
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {
-            const uint64_t bits = tb_body(cb0 + kColBytes * (tlo >> 4), loc, gbase);
+            const uint64_t bits = tb48(cb0 + kColBytes * (tlo >> 4), loc);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
@@ -394,7 +452,7 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb_body(cb0 + kColBytes * (tlo >> 4), loc, gbase));
+                put_bits48(ob, tlo, tb48(cb0 + kColBytes * (tlo >> 4), loc));
             }
             fin = loc;
             fixed = true;
