@@ -71,6 +71,8 @@
 // until all are proven.  So the output is exactly the reference's for every input; only
 // the time depends on how fast survivor paths merge.
 
+#include <type_traits>
+
 #include "vtb_k7_common.h"
 
 namespace vtb {
@@ -556,7 +558,10 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     // (V, W) of a slot from two unrelated VGPRs by ds_write2_b32 (a ds_write_b64 would need
     // them in a register pair: 8 moves per chunk); three bases keep offsets below 256 dwords.
     const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
-    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
+    // PADCHK: the chunk may hold padding rows (only the chunk containing step T; the ACS
+    // loop is split so that the check stays out of its other iterations).
+    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4], auto padchk) {
+        constexpr bool PADCHK = decltype(padchk)::value;
         uint2* col = reinterpret_cast<uint2*>(tab) + srow;  // column k at col[kCol * k]
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
@@ -565,7 +570,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
 #undef VTB_W2
-        if ((c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows (last chunk only)
+        if (PADCHK && (c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows
             constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     auto stage = [&](int c, uint32_t ra, uint32_t rb) {
         uint32_t e[4], et[4];
         stage_compute(ra, rb, e, et, true);
-        stage_write(c, e, et);
+        stage_write(c, e, et, std::true_type{});
     };
 
     uint32_t M = (lane == 0) ? H::BIAS * kR1 : (H::BIAS + H::SC * INIT) * kR1;
@@ -604,7 +609,9 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
     const int tacs = (dbg & 2) ? 0 : Tpad;
-    for (int t0 = tbeg; t0 < tacs; t0 += kChunk) {
+    // One 48-step chunk of the ACS (fully unrolled); PADTAG: this chunk stages the chunk that
+    // holds step T (padding rows possible).
+    auto acs_chunk = [&](const int t0, auto padtag) __attribute__((always_inline)) {
         const int c0 = t0 / kChunk;
         const uint2* ap[6];
 #pragma unroll
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         if ((G) == 0) load_raw(c0 + 1, ra, rb);                                                   \
         if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set, false);                            \
         if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
-            stage_write(c0 + 1, se, set);                                                         \
+            stage_write(c0 + 1, se, set, padtag);                                                 \
         }                                                                                         \
         uint2* cur = buf[(G) & 3];                                                                \
         /* table reads AH groups ahead, issued after the two permlane steps */                     \
@@ -682,6 +689,17 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 #undef VTB_RENORM_READ
 #undef VTB_RENORM_APPLY
 #undef VTB_RD
+    };
+    {
+        // chunks in order; only the one before the last stages padding rows
+        const int tstage = tacs - 2 * kChunk;  // the chunk that stages the last one
+        int t0 = tbeg;
+        for (; t0 < tstage; t0 += kChunk) acs_chunk(t0, std::false_type{});
+        if (t0 == tstage) {
+            acs_chunk(t0, std::true_type{});
+            t0 += kChunk;
+        }
+        if (t0 < tacs) acs_chunk(t0, std::false_type{});
     }
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
