@@ -116,6 +116,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.out_stride = out_stride;
     a.frames = frames;
     a.stream = stream;
+    a.cus = p->cus;
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
     const char* force = std::getenv("VTB_KERNEL");
     const bool any = !force || !*force;

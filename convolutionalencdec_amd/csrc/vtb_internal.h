@@ -24,11 +24,13 @@ struct Launch {
     size_t frames = 0;
     hipStream_t stream = nullptr;
     void* ws = nullptr;  // device workspace of at least *_workspace_bytes() (plan-owned)
+    int cus = 256;       // compute units of the device (persistent grids)
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
 // Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
-// kernel: bit 2 skip traceback verification, bit 3 warm-up walk only).  Never
+// kernel: bit 2 skip traceback verification, bit 3 warm-up walk only, bit 4 return at entry, bit 5
+// one wave per frame pair instead of the persistent grid).  Never
 // set in production; outputs are garbage when set.
 inline int debug_flags() {
     const char* v = getenv("VTB_DEBUG");

@@ -367,9 +367,9 @@ __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint3
 // step e_f (no merge within sa.ring steps) the frame is flagged: -1 bits until last.
 template <bool SOFT>
 __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
-                                 uint64_t gbase, size_t fa, bool has_b) {
+                                 uint64_t gbase, size_t fa, bool has_b, size_t wp) {
     const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
-    uint32_t* st = sa.state + size_t(blockIdx.x) * kStreamStateWords;
+    uint32_t* st = sa.state + wp * kStreamStateWords;
     const int e0 = int(st[64 + f]);  // this lane's frame
     const uint32_t flags0 = __builtin_amdgcn_readfirstlane(st[66]);
     const bool real = f == 0 || has_b;
@@ -453,17 +453,53 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
 }
 
 // GS = false: survivor words in LDS at [r0, r0 + 16 Tpad).  GS = true: survivor words in a
-// global workspace, 16 Tpad bytes per wave at ws + blockIdx.x * ws_wave (same addressing with
+// global workspace, 16 Tpad bytes per wave at ws + slot * ws_wave (same addressing with
 // r0 = 0), for frames whose survivors do not fit in LDS or would cut the occupancy.
 // STREAM (with GS): one call of the streaming decoder (vtb_stream_decode): steps
 // [sa.t_begin, Tpad = sa.t_end) continue from the metrics in sa.state, survivor words go to a
 // ring of sa.ring steps, and the traceback emits the bits that became final (see
 // stream_traceback below).
+// Per phase: byte offset of the lane's (V, W) column in the table ring: its edge label c
+// and R = bit p of its location (the same for every frame pair of the wave).
+__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[6]) {
+    const int loc = int(lane_of(threadIdx.x));
+#pragma unroll
+    for (int ph = 0; ph < 6; ph++) {
+        const int p = 5 - ph;
+        off[ph] = 8u * kCol * (table.symm[rotl6(loc & ~(1 << p), ph)] + 4u * ((loc >> p) & 1u));
+    }
+}
+
+// Raw input of chunk 0 of pair wp (load_raw(0) below, for the persistent loop's prefetch of
+// the next pair during this pair's traceback).  Issued in asm, waited for by stage_compute.
+template <bool SOFT>
+__device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, size_t frames, int T, size_t wp,
+                                          uint32_t& ra, uint32_t& rb) {
+    const int lane = threadIdx.x, srow = lane < kChunk ? lane : lane - kChunk;
+    const size_t fa = 2 * wp, fb = fa + 1 < frames ? fa + 1 : fa;
+    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(in + fa * in_stride));
+    const uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(in + fb * in_stride));
+    const uint32_t tc = uint32_t(srow < T ? srow : T - 1);
+    if constexpr (SOFT) {
+        asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
+                     : "=&v"(ra), "=&v"(rb) : "v"(2 * tc), "s"(baseA), "s"(baseB));
+    } else {
+        asm volatile("global_load_ubyte %0, %2, %3\n\tglobal_load_ubyte %1, %2, %4"
+                     : "=&v"(ra), "=&v"(rb) : "v"(tc), "s"(baseA), "s"(baseB));
+    }
+}
+
+// One frame pair (wave-pair index wp: frames 2wp, 2wp + 1); slot = this wave's survivor
+// workspace (GS).  pre: chunk 0's raw input is already in (pra, prb); next: the pair this wave
+// decodes after this one (its chunk 0 is prefetched into (pra, prb) before the traceback;
+// LDS variant only, whose traceback issues no global loads that would wait behind it).
+
 template <bool SOFT, bool GS, bool STREAM>
-__global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
-                                                    uint8_t* __restrict__ out, size_t out_stride, int T, int L,
-                                                    int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
-                                                    uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
+__device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
+                                        size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
+                                        int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
+                                        const StreamArgs& sa, size_t wp, size_t slot, bool pre, size_t next,
+                                        uint32_t& pra, uint32_t& prb, const uint32_t (&off)[6]) {
     static_assert(GS || !STREAM, "the streaming decoder keeps its survivors in a global ring");
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
@@ -473,23 +509,12 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     uint8_t* tab = smem;
     uint32_t* dec = reinterpret_cast<uint32_t*>(smem + r0);
     const int lane = threadIdx.x;
-    const size_t fa = (size_t)blockIdx.x * 2, fb = fa + 1;
+    if (dbg & 16) return;  // measurement only: launch cost
+    const size_t fa = wp * 2, fb = fa + 1;
     const bool has_b = fb < frames;
-    const uint64_t gbase = GS ? uniform64(reinterpret_cast<uint64_t>(ws + blockIdx.x * ws_wave)) : 0;
+    const uint64_t gbase = GS ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
     const uint8_t* inA = in + fa * in_stride;
     const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
-
-    // Per phase: byte offset of the lane's (V, W) column in the table ring: its edge label c
-    // and R = bit p of its location.
-    uint32_t off[6];
-    {
-        const int loc = int(lane_of(lane));
-#pragma unroll
-        for (int ph = 0; ph < 6; ph++) {
-            const int p = 5 - ph;
-            off[ph] = 8u * kCol * (table.symm[rotl6(loc & ~(1 << p), ph)] + 4u * ((loc >> p) & 1u));
-        }
-    }
 
     // Table staging: lane r < 48 builds the row of step 48c + r from the raw input bytes of
     // that step (soft q0 | q1 << 8, hard the byte).  The loads are issued in asm at the start
@@ -590,11 +615,15 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     // first step of this launch: 0, or (streaming) where the previous call stopped
     const int tbeg = STREAM ? sa.t_begin : 0;
     if constexpr (STREAM) {
-        if (tbeg > 0) M = sa.state[size_t(blockIdx.x) * kStreamStateWords + lane];
+        if (tbeg > 0) M = sa.state[wp * kStreamStateWords + lane];
     }
     uint32_t ra = 0, rb = 0;
     if (!STREAM || Tpad > tbeg) {  // (a streaming call may have no new step)
-        load_raw(tbeg / kChunk, ra, rb);
+        if (pre) {
+            ra = pra, rb = prb;
+        } else {
+            load_raw(tbeg / kChunk, ra, rb);
+        }
         stage(tbeg / kChunk, ra, rb);
     }
     // software pipeline: the table pairs of group G+3 are read while group G computes, into
@@ -704,10 +733,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
     if constexpr (STREAM) {
-        if (!sa.last) sa.state[size_t(blockIdx.x) * kStreamStateWords + lane] = M;
-        stream_traceback<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b);
+        if (!sa.last) sa.state[wp * kStreamStateWords + lane] = M;
+        stream_traceback<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp);
         return;
     }
+    if (!GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
     if (dbg & 1) return;
 
     // ---------------- traceback: verified block-parallel chains ----------------
@@ -774,48 +804,86 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             for (int i = lane; i < nbytes; i += 64) o2[i] = tab[4 * tbb + i];
         }
     }
+    // the prefetched registers are complete before they leave this function (no copy of an
+    // in-flight load destination can happen past here)
+    if (!GS && next < (frames + 1) / 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+}
+
+// Persistent over frame pairs: wave b decodes pairs b, b + grid, ... (the grid is what the
+// CUs hold at once, so every SIMD keeps the same number of waves to the end instead of the
+// dispatcher refilling freed slots unevenly; the streaming decoder launches one wave per
+// pair).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
+template <bool SOFT, bool GS, bool STREAM>
+__global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                    uint8_t* __restrict__ out, size_t out_stride, int T, int L,
+                                                    int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
+                                                    uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
+    const size_t pairs = (frames + 1) / 2;
+    uint32_t pra = 0, prb = 0;  // next pair's chunk-0 input, prefetched during the traceback (LDS variant)
+    uint32_t off[6];
+    column_offsets(table, off);
+    for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
+        k7_pair<SOFT, GS, STREAM>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws, ws_wave,
+                                  sa, wp, STREAM ? wp : size_t(blockIdx.x), !GS && wp != blockIdx.x,
+                                  wp + gridDim.x, pra, prb, off);
+        __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
+    }
 }
 
 // LDS of the survivor-in-global variant: table ring and decoded bytes only.
 size_t lds_bytes_gs(int T) { return (size_t)region0(T); }
 size_t ws_wave_bytes(int T) { return 16 * (size_t)t_pad(T); }
-constexpr size_t kMaxWsBytes = size_t(1) << 30;  // workspace per launch slab
+constexpr size_t kMaxWsBytes = size_t(1) << 30;  // survivor workspace cap (global variant)
 
-// Waves (frame pairs) per launch of the global variant: the whole batch, unless its
-// workspace would exceed kMaxWsBytes; then the batch runs as several launches over one
-// workspace (stream-ordered).
-size_t slab_waves(const Launch& a) {
-    const size_t waves = (a.frames + 1) / 2;
-    size_t slab = kMaxWsBytes / ws_wave_bytes(a.T);
-    if (slab < 1) slab = 1;
-    return slab < waves ? slab : waves;
+template <bool GS>
+size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T) : lds_bytes(a.T); }
+
+template <bool GS>
+auto kernel_of(const Launch& a) {
+    return a.soft ? k7_lds_kernel<true, GS, false> : k7_lds_kernel<false, GS, false>;
+}
+
+// Persistent grid: the frame pairs, at most what the CUs hold at once (occupancy of this
+// kernel and LDS size), and for the global variant at most kMaxWsBytes of survivor slots.
+template <bool GS>
+size_t grid_waves(const Launch& a) {
+    const size_t pairs = (a.frames + 1) / 2;
+    const size_t lds = lds_of<GS>(a);
+    auto kern = kernel_of<GS>(a);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(lds));
+    int per_cu = 0;
+    size_t grid = pairs;
+    if (!(debug_flags() & 32) &&  // VTB_DEBUG bit 5 (measurement only): one wave per pair
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) == hipSuccess && per_cu > 0) {
+        const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
+        if (resident < grid) grid = resident;
+    }
+    if (GS) {
+        size_t cap = kMaxWsBytes / ws_wave_bytes(a.T);
+        if (cap < 1) cap = 1;
+        if (cap < grid) grid = cap;
+    }
+    return grid;
 }
 
 template <bool GS>
 hipError_t launch_k7(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (GS && !a.ws) return hipErrorInvalidValue;
-    const size_t lds = GS ? lds_bytes_gs(a.T) : lds_bytes(a.T);
-    auto kern = a.soft ? k7_lds_kernel<true, GS, false> : k7_lds_kernel<false, GS, false>;
+    const size_t lds = lds_of<GS>(a);
+    auto kern = kernel_of<GS>(a);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    const size_t waves = (a.frames + 1) / 2;
-    const size_t slab = GS ? slab_waves(a) : waves;
-    const int dbg = debug_flags();
-    for (size_t w0 = 0; w0 < waves; w0 += slab) {
-        const size_t nw = waves - w0 < slab ? waves - w0 : slab;
-        const size_t f0 = 2 * w0;
-        const size_t nf = a.frames - f0 < 2 * nw ? a.frames - f0 : 2 * nw;
-        hipLaunchKernelGGL(kern, dim3(unsigned(nw)), dim3(64), lds, a.stream, a.in + f0 * a.in_stride, a.in_stride,
-                           a.out + f0 * a.out_stride, a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T),
-                           nf, dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    const size_t grid = grid_waves<GS>(a);
+    hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
+                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), a,
+                       static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -828,7 +896,7 @@ hipError_t launch_k7_lds(const Launch& a) { return launch_k7<false>(a); }
 
 bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T) <= 160 * 1024; }
 
-size_t k7_global_workspace_bytes(const Launch& a) { return slab_waves(a) * ws_wave_bytes(a.T); }
+size_t k7_global_workspace_bytes(const Launch& a) { return grid_waves<true>(a) * ws_wave_bytes(a.T); }
 
 hipError_t launch_k7_global(const Launch& a) { return launch_k7<true>(a); }
 
