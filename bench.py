@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: step i runs on stream i mod inflight (own plan and output), so one "
                          "batch's tail overlaps the next one's start")
+    ap.add_argument("--graph", action="store_true",
+                    help="launch the K timed steps as one captured HIP graph (K kernel nodes, one batch each) "
+                         "instead of K separate launches")
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="measure the streaming decoder (vtb_stream_*, SURVEY.md 8 f3) instead: every stream "
                          "receives this many segments per step, one long frame per stream")
@@ -300,7 +303,18 @@ def main():
     # timed region's K back-to-back launches (what rocprofv3's per-kernel average sees).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
-    elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    if args.graph and nin == 1:
+        # the K steps captured as K kernel nodes of one graph (same batch, same output buffer)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(args.steps):
+                dec.decode_device(x, out=out)
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(out.cpu(), torch.from_numpy(decoded))
+        elapsed = timer.run(graph.replay, 1, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    else:
+        elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     def step():  # noqa: F811 -- single-stream launches (per-launch duration with --inflight > 1)
@@ -373,6 +387,7 @@ def main():
             "global_batch_frames": F * world,
             "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
             "batches_in_flight": nin,
+            "graph": bool(args.graph and nin == 1),
             "host_buffers_mbps": host_mbps,
             "decoded_ber": ber,
         },
