@@ -211,27 +211,10 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
     o[2] = (unsigned short)((rh >> 24) | ((rh >> 8) & 0xff00u));
 }
 
-template <bool SOFT>
-__global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
-                                                uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
-                                                int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
-                                                uint8_t* __restrict__ ws, size_t ws_wave) {
-    constexpr uint32_t Q = SOFT ? 255 : 1;
-    using H = Hist<SOFT>;
-    constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
-    extern __shared__ uint4 smem4[];
-    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
-    const int lane = threadIdx.x;
-    const size_t fa = (size_t)blockIdx.x * 2, fb = fa + 1;
-    const bool has_b = fb < frames;
-    const uint8_t* inA = in + fa * in_stride;
-    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;
-    const uint64_t gbase = uniform64(reinterpret_cast<uint64_t>(ws + blockIdx.x * ws_wave));
-    const uint32_t lam = lane_of(lane);  // this lane's 6 low location bits
-
-    // Per register and phase: byte offset of the (V, W) column (edge label c of the
-    // butterfly's upper state, R = bit p of the location).
-    uint32_t off[4][8];
+// Per register and phase: byte offset of the (V, W) column (edge label c of the butterfly's
+// upper state, R = bit p of the location); the same for every frame pair of the wave.
+__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[4][8]) {
+    const uint32_t lam = lane_of(threadIdx.x);
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -239,6 +222,27 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
             const int l = r * 64 + int(lam), p = 7 - ph;
             off[r][ph] = 8u * kCol * (table.symm[rotl8(l & ~(1 << p), ph)] + 4u * ((l >> p) & 1u));
         }
+}
+
+// One frame pair (wave-pair index wp: frames 2wp, 2wp + 1), survivors in workspace slot
+// `slot` (this wave's).
+template <bool SOFT>
+__device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
+                                        size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
+                                        size_t frames, int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t wp,
+                                        size_t slot, const uint32_t (&off)[4][8]) {
+    constexpr uint32_t Q = SOFT ? 255 : 1;
+    using H = Hist<SOFT>;
+    constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
+    extern __shared__ uint4 smem4[];
+    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
+    const int lane = threadIdx.x;
+    const size_t fa = wp * 2, fb = fa + 1;
+    const bool has_b = fb < frames;
+    const uint8_t* inA = in + fa * in_stride;
+    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;
+    const uint64_t gbase = uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave));
+    const uint32_t lam = lane_of(lane);  // this lane's 6 low location bits
 
     // Table staging (as vtb_k7_lds.hip): lane r < 48 builds ring row r of a chunk from the
     // raw input of kernel step 48c + r, i.e. input step 48c + r - delta.
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     // Soft input, padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping
     // decisions (both history bits = the location's own bits t_even mod 8, +1 of l').
     if (SOFT && !(dbg & 2)) {
-        uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + blockIdx.x * ws_wave);
+        uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + slot * ws_wave);
         for (int g = Tq >> 4; g < (Tpad >> 4); g++) {
             const int w0 = Tq > 16 * g ? (Tq - 16 * g) >> 1 : 0;  // first padding window of the word
 #pragma unroll
@@ -471,11 +475,38 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     }
 }
 
-size_t slab_waves(const Launch& a, int Tq) {
-    const size_t waves = (a.frames + 1) / 2;
-    size_t slab = (size_t(1) << 30) / ws_wave_bytes(Tq);
-    if (slab < 1) slab = 1;
-    return slab < waves ? slab : waves;
+// Persistent over frame pairs (as vtb_k7_lds.hip): wave b decodes pairs b, b + grid, ...
+template <bool SOFT>
+__global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
+                                                int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
+                                                uint8_t* __restrict__ ws, size_t ws_wave) {
+    uint32_t off[4][8];
+    column_offsets(table, off);
+    const size_t pairs = (frames + 1) / 2;
+    for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
+        k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, wp,
+                      blockIdx.x, off);
+        __syncthreads();  // LDS (decoded bytes) before the next pair's table ring
+    }
+}
+
+// Grid: the frame pairs, at most what the CUs hold at once and at most 1 GiB of survivor
+// slots (one per wave).
+size_t grid_waves(const Launch& a, int Tq) {
+    const size_t pairs = (a.frames + 1) / 2;
+    size_t grid = pairs;
+    auto kern = a.soft ? k9_kernel<true> : k9_kernel<false>;
+    int per_cu = 0;
+    if (!(debug_flags() & 32) &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, (size_t)region0(Tq)) == hipSuccess &&
+        per_cu > 0) {
+        const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
+        if (resident < grid) grid = resident;
+    }
+    size_t cap = (size_t(1) << 30) / ws_wave_bytes(Tq);
+    if (cap < 1) cap = 1;
+    return cap < grid ? cap : grid;
 }
 
 }  // namespace
@@ -486,7 +517,7 @@ bool k9_supported(const Launch& a) {
 
 size_t k9_workspace_bytes(const Launch& a) {
     const int Tq = a.T + (a.T & 1);
-    return slab_waves(a, Tq) * ws_wave_bytes(Tq);
+    return grid_waves(a, Tq) * ws_wave_bytes(Tq);
 }
 
 hipError_t launch_k9(const Launch& a) {
@@ -500,19 +531,11 @@ hipError_t launch_k9(const Launch& a) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    const size_t waves = (a.frames + 1) / 2;
-    const size_t slab = slab_waves(a, Tq);
-    const int dbg = debug_flags();
-    for (size_t w0 = 0; w0 < waves; w0 += slab) {
-        const size_t nw = waves - w0 < slab ? waves - w0 : slab;
-        const size_t f0 = 2 * w0;
-        const size_t nf = a.frames - f0 < 2 * nw ? a.frames - f0 : 2 * nw;
-        hipLaunchKernelGGL(kern, dim3(unsigned(nw)), dim3(64), lds, a.stream, a.in + f0 * a.in_stride, a.in_stride,
-                           a.out + f0 * a.out_stride, a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), nf,
-                           dbg, a, static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq));
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
+    hipLaunchKernelGGL(kern, dim3(unsigned(grid_waves(a, Tq))), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
+                       static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     return hipSuccess;
 }
 
