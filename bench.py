@@ -331,15 +331,18 @@ def main():
 
     # PCIe-inclusive rate: the same batch from pageable host memory through
     # vtb_decode_host (H2D copy, decode, D2H copy, synchronise); reported beside, never `value`.
+    # Every rank at once (each GPU has its own PCIe link): aggregate over ranks, slowest rank.
     host_mbps = None
-    if args.gen == "host" and world == 1:
+    if args.gen == "host":
         rx_host = np.ascontiguousarray(rx.reshape(F, -1))
         dec.decode_host(rx_host)
         reps = 10
+        barrier()
         th = time.perf_counter()
         for _ in range(reps):
             dec.decode_host(rx_host)
-        host_mbps = round(F * L * reps / (time.perf_counter() - th) / 1e6, 1)
+        host_s = allreduce_max(time.perf_counter() - th)
+        host_mbps = round(world * F * L * reps / host_s / 1e6, 1)
 
     ms_per_step = elapsed / args.steps * 1e3
     total_bits = F * L * world

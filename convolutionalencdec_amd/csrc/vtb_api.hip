@@ -224,6 +224,28 @@ hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream) {
     return hipMallocFromPoolAsync(p, bytes, pool, stream);
 }
 
+int resident_per_cu(const void* kernel, size_t lds) {
+    struct Entry {
+        const void* k;
+        size_t lds;
+        int dev, n;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const Entry& e : cache)
+            if (e.k == kernel && e.lds == lds && e.dev == dev) return e.n;
+    }
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 64, lds) != hipSuccess || n < 0) n = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    cache.push_back({kernel, lds, dev, n});
+    return n;
+}
+
 hipError_t workspace_free(void* p, hipStream_t stream) { return hipFreeAsync(p, stream); }
 
 }  // namespace vtb

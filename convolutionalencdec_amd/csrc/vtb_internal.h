@@ -37,6 +37,11 @@ inline int debug_flags() {
     return v ? atoi(v) : 0;
 }
 
+// Resident blocks per CU of a 64-thread kernel with `lds` bytes of dynamic LDS
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor, cached: the query costs host time on every
+// launch otherwise).  0 if unknown.
+int resident_per_cu(const void* kernel, size_t lds);
+
 // Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
 // shape limits are reported through *_supported() beforehand.
 bool lds_path_supported(const Launch& a);

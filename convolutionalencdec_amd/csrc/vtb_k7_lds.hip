@@ -494,7 +494,7 @@ __device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, s
 // decodes after this one (its chunk 0 is prefetched into (pra, prb) before the traceback;
 // LDS variant only, whose traceback issues no global loads that would wait behind it).
 
-template <bool SOFT, bool GS, bool STREAM>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP>
 __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
@@ -619,7 +619,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     }
     uint32_t ra = 0, rb = 0;
     if (!STREAM || Tpad > tbeg) {  // (a streaming call may have no new step)
-        if (pre) {
+        if (LOOP && pre) {
             ra = pra, rb = prb;
         } else {
             load_raw(tbeg / kChunk, ra, rb);
@@ -737,7 +737,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         stream_traceback<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp);
         return;
     }
-    if (!GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
+    if (LOOP && !GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
     if (dbg & 1) return;
 
     // ---------------- traceback: verified block-parallel chains ----------------
@@ -806,27 +806,34 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     }
     // the prefetched registers are complete before they leave this function (no copy of an
     // in-flight load destination can happen past here)
-    if (!GS && next < (frames + 1) / 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+    if (LOOP && !GS && next < (frames + 1) / 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
 }
 
-// Persistent over frame pairs: wave b decodes pairs b, b + grid, ... (the grid is what the
-// CUs hold at once, so every SIMD keeps the same number of waves to the end instead of the
-// dispatcher refilling freed slots unevenly; the streaming decoder launches one wave per
-// pair).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
-template <bool SOFT, bool GS, bool STREAM>
+// LOOP: persistent over frame pairs, wave b decodes pairs b, b + grid, ... (the grid is what
+// the CUs hold at once, so every SIMD keeps the same number of waves to the end instead of
+// the dispatcher refilling freed slots unevenly).  !LOOP: one wave per pair, for batches the
+// CUs hold in one round and for the streaming decoder (the loop's extra live state costs
+// ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
+template <bool SOFT, bool GS, bool STREAM, bool LOOP>
 __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
                                                     uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
+    static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
     const size_t pairs = (frames + 1) / 2;
     uint32_t pra = 0, prb = 0;  // next pair's chunk-0 input, prefetched during the traceback (LDS variant)
     uint32_t off[6];
     column_offsets(table, off);
-    for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
-        k7_pair<SOFT, GS, STREAM>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws, ws_wave,
-                                  sa, wp, STREAM ? wp : size_t(blockIdx.x), !GS && wp != blockIdx.x,
-                                  wp + gridDim.x, pra, prb, off);
-        __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
+    if constexpr (!LOOP) {
+        k7_pair<SOFT, GS, STREAM, false>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
+                                         ws_wave, sa, blockIdx.x, blockIdx.x, false, pairs, pra, prb, off);
+    } else {
+        for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
+            k7_pair<SOFT, GS, STREAM, true>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
+                                            ws_wave, sa, wp, blockIdx.x, !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb,
+                                            off);
+            __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
+        }
     }
 }
 
@@ -838,9 +845,9 @@ constexpr size_t kMaxWsBytes = size_t(1) << 30;  // survivor workspace cap (glob
 template <bool GS>
 size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T) : lds_bytes(a.T); }
 
-template <bool GS>
+template <bool GS, bool LOOP = true>
 auto kernel_of(const Launch& a) {
-    return a.soft ? k7_lds_kernel<true, GS, false> : k7_lds_kernel<false, GS, false>;
+    return a.soft ? k7_lds_kernel<true, GS, false, LOOP> : k7_lds_kernel<false, GS, false, LOOP>;
 }
 
 // Persistent grid: the frame pairs, at most what the CUs hold at once (occupancy of this
@@ -853,10 +860,10 @@ size_t grid_waves(const Launch& a) {
     if (lds > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(lds));
-    int per_cu = 0;
     size_t grid = pairs;
-    if (!(debug_flags() & 32) &&  // VTB_DEBUG bit 5 (measurement only): one wave per pair
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) == hipSuccess && per_cu > 0) {
+    const int per_cu = (debug_flags() & 32) ? 0  // VTB_DEBUG bit 5 (measurement only): one wave per pair
+                                             : resident_per_cu(reinterpret_cast<const void*>(kern), lds);
+    if (per_cu > 0) {
         const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
         if (resident < grid) grid = resident;
     }
@@ -873,13 +880,13 @@ hipError_t launch_k7(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (GS && !a.ws) return hipErrorInvalidValue;
     const size_t lds = lds_of<GS>(a);
-    auto kern = kernel_of<GS>(a);
+    const size_t grid = grid_waves<GS>(a);
+    auto kern = grid < (a.frames + 1) / 2 ? kernel_of<GS, true>(a) : kernel_of<GS, false>(a);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    const size_t grid = grid_waves<GS>(a);
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
                        a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), a,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
@@ -906,7 +913,7 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s) {
     if (a.frames == 0) return hipSuccess;
     if (!a.ws || !s.state || !s.out_bits || s.ring < 48 || s.ring % 48 || s.t_begin % 48 || s.t_end % 48)
         return hipErrorInvalidValue;
-    auto kern = a.soft ? k7_lds_kernel<true, true, true> : k7_lds_kernel<false, true, true>;
+    auto kern = a.soft ? k7_lds_kernel<true, true, true, false> : k7_lds_kernel<false, true, true, false>;
     const size_t lds = (kRingBytes + 255) / 256 * 256;
     const size_t waves = (a.frames + 1) / 2;
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,

@@ -497,10 +497,9 @@ size_t grid_waves(const Launch& a, int Tq) {
     const size_t pairs = (a.frames + 1) / 2;
     size_t grid = pairs;
     auto kern = a.soft ? k9_kernel<true> : k9_kernel<false>;
-    int per_cu = 0;
-    if (!(debug_flags() & 32) &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, (size_t)region0(Tq)) == hipSuccess &&
-        per_cu > 0) {
+    const int per_cu =
+        (debug_flags() & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq));
+    if (per_cu > 0) {
         const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
         if (resident < grid) grid = resident;
     }

@@ -101,6 +101,26 @@ def test_soft_random_vs_oracle(orc, K, L, kernel):
 
 
 @pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("K,L,F", [(7, 1024, 12289), (7, 1024, 40961), (9, 512, 20481)])
+def test_persistent_grid_many_pairs_per_wave(orc, K, L, F, soft, kernel):
+    """Batches with several frame pairs per wave of the persistent grid (more pairs than the
+    CUs hold at once), an odd frame count (the last pair has one frame), the next pair's
+    input prefetched during a traceback: the whole batch against the oracle."""
+    from convolutionalencdec_amd import frames as devframes
+
+    kernel.need(K)
+    if kernel == "lds" or (kernel == "k7" and F > 20000):
+        pytest.skip("covered at smaller sizes for this kernel family")
+    code = ConvCode(K, CODES[K])
+    unc, rx = devframes.make_frames(code, F, L, soft=soft, snr_db=-4.0, p=0.04, seed=F + K)
+    d = ViterbiDecoder(code, frame_bits=L, soft=soft)
+    got = d.decode_device(rx.reshape(F, -1)).cpu().numpy()
+    ref = orc.decode(K, CODES[K], rx.reshape(F, -1).cpu().numpy(), L, soft=soft, threads=min(16, os.cpu_count() or 1))
+    bad = np.flatnonzero((got != ref).any(axis=1))
+    assert bad.size == 0, (bad.size, bad[:8])
+
+
+@pytest.mark.parametrize("soft", [False, True])
 @pytest.mark.parametrize("L", [10000, 16384])
 def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
     """Frames past the LDS-resident kernel's survivor capacity up to the API maximum
