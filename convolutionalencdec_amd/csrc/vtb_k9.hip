@@ -475,19 +475,25 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     }
 }
 
-// Persistent over frame pairs (as vtb_k7_lds.hip): wave b decodes pairs b, b + grid, ...
-template <bool SOFT>
+// LOOP: persistent over frame pairs (as vtb_k7_lds.hip), wave b decodes pairs b, b + grid, ...;
+// !LOOP: one wave per pair, for batches the CUs hold in one round (fewer live registers).
+template <bool SOFT, bool LOOP>
 __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                 uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
                                                 int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
                                                 uint8_t* __restrict__ ws, size_t ws_wave) {
     uint32_t off[4][8];
     column_offsets(table, off);
-    const size_t pairs = (frames + 1) / 2;
-    for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
-        k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, wp,
+    if constexpr (!LOOP) {
+        k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, blockIdx.x,
                       blockIdx.x, off);
-        __syncthreads();  // LDS (decoded bytes) before the next pair's table ring
+    } else {
+        const size_t pairs = (frames + 1) / 2;
+        for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
+            k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, wp,
+                          blockIdx.x, off);
+            __syncthreads();  // LDS (decoded bytes) before the next pair's table ring
+        }
     }
 }
 
@@ -496,7 +502,7 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
 size_t grid_waves(const Launch& a, int Tq) {
     const size_t pairs = (a.frames + 1) / 2;
     size_t grid = pairs;
-    auto kern = a.soft ? k9_kernel<true> : k9_kernel<false>;
+    auto kern = a.soft ? k9_kernel<true, true> : k9_kernel<false, true>;
     const int per_cu =
         (debug_flags() & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq));
     if (per_cu > 0) {
@@ -524,13 +530,15 @@ hipError_t launch_k9(const Launch& a) {
     if (!a.ws) return hipErrorInvalidValue;
     const int delta = a.T & 1, Tq = a.T + delta;
     const size_t lds = (size_t)region0(Tq);
-    auto kern = a.soft ? k9_kernel<true> : k9_kernel<false>;
+    const size_t grid = grid_waves(a, Tq);
+    auto kern = grid < (a.frames + 1) / 2 ? (a.soft ? k9_kernel<true, true> : k9_kernel<false, true>)
+                                          : (a.soft ? k9_kernel<true, false> : k9_kernel<false, false>);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(unsigned(grid_waves(a, Tq))), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
+    hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq));
     const hipError_t e = hipGetLastError();
