@@ -32,6 +32,8 @@ struct vtb_plan {
     uint8_t* d_out = nullptr;
     size_t cap_frames = 0;
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // host path: copies of one chunk overlap the next's decode
+    std::vector<hipEvent_t> events;     // host path: per chunk, H2D done and decode done
     // kernel workspace (survivor words), stream-ordered pool memory, grown on demand
     void* ws = nullptr;
     size_t ws_bytes = 0;
@@ -341,6 +343,8 @@ void vtb_plan_destroy(vtb_plan_t* plan) {
         (void)vtb::workspace_free(plan->ws, nullptr);
         (void)hipStreamSynchronize(nullptr);
     }
+    for (hipEvent_t e : plan->events) (void)hipEventDestroy(e);
+    if (plan->copy_stream) (void)hipStreamDestroy(plan->copy_stream);
     if (plan->stream) (void)hipStreamDestroy(plan->stream);
     delete plan;
 }
@@ -375,13 +379,49 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
         if (hipMalloc(&plan->d_out, frames * ob) != hipSuccess) return VTB_ERR_NOMEM;
         plan->cap_frames = frames;
     }
-    if (hipMemcpyAsync(plan->d_in, h_in, frames * ib, hipMemcpyHostToDevice, plan->stream) != hipSuccess)
+    // Large batches in chunks: the H2D copy of chunk i + 1 (copy stream) overlaps the decode of
+    // chunk i (plan stream); every output copy follows its chunk's decode.  Small batches (one
+    // launch round) in one piece.
+    const size_t kChunkFrames = 16384;
+    const size_t nch = frames <= 2 * kChunkFrames ? 1 : (frames + kChunkFrames - 1) / kChunkFrames;
+    if (nch == 1) {
+        if (hipMemcpyAsync(plan->d_in, h_in, frames * ib, hipMemcpyHostToDevice, plan->stream) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        int e = launch(plan, plan->d_in, ib, plan->d_out, ob, frames, plan->stream);
+        if (e != VTB_OK) return e;
+        if (hipMemcpyAsync(h_out, plan->d_out, frames * ob, hipMemcpyDeviceToHost, plan->stream) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        return hipStreamSynchronize(plan->stream) == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
+    }
+    if (!plan->copy_stream && hipStreamCreateWithFlags(&plan->copy_stream, hipStreamNonBlocking) != hipSuccess)
         return VTB_ERR_DEVICE;
-    int e = launch(plan, plan->d_in, ib, plan->d_out, ob, frames, plan->stream);
-    if (e != VTB_OK) return e;
-    if (hipMemcpyAsync(h_out, plan->d_out, frames * ob, hipMemcpyDeviceToHost, plan->stream) != hipSuccess)
-        return VTB_ERR_DEVICE;
-    return hipStreamSynchronize(plan->stream) == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
+    while (plan->events.size() < 2 * nch) {
+        hipEvent_t ev;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return VTB_ERR_DEVICE;
+        plan->events.push_back(ev);
+    }
+    for (size_t i = 0; i < nch; i++) {
+        const size_t lo = i * kChunkFrames, n = frames - lo < kChunkFrames ? frames - lo : kChunkFrames;
+        hipEvent_t copied = plan->events[2 * i], decoded = plan->events[2 * i + 1];
+        if (hipMemcpyAsync(plan->d_in + lo * ib, h_in + lo * ib, n * ib, hipMemcpyHostToDevice, plan->copy_stream) !=
+                hipSuccess ||
+            hipEventRecord(copied, plan->copy_stream) != hipSuccess ||
+            hipStreamWaitEvent(plan->stream, copied, 0) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        int e = launch(plan, plan->d_in + lo * ib, ib, plan->d_out + lo * ob, ob, n, plan->stream);
+        if (e != VTB_OK) return e;
+        if (hipEventRecord(decoded, plan->stream) != hipSuccess) return VTB_ERR_DEVICE;
+    }
+    for (size_t i = 0; i < nch; i++) {
+        const size_t lo = i * kChunkFrames, n = frames - lo < kChunkFrames ? frames - lo : kChunkFrames;
+        if (hipStreamWaitEvent(plan->copy_stream, plan->events[2 * i + 1], 0) != hipSuccess ||
+            hipMemcpyAsync(h_out + lo * ob, plan->d_out + lo * ob, n * ob, hipMemcpyDeviceToHost,
+                           plan->copy_stream) != hipSuccess)
+            return VTB_ERR_DEVICE;
+    }
+    return hipStreamSynchronize(plan->copy_stream) == hipSuccess && hipStreamSynchronize(plan->stream) == hipSuccess
+               ? VTB_OK
+               : VTB_ERR_DEVICE;
 }
 
 int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,

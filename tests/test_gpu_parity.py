@@ -216,6 +216,24 @@ def test_k9_full_config(orc, kernel):
     assert ber < 1e-3
 
 
+@pytest.mark.parametrize("soft", [False, True])
+def test_host_path_chunked(orc, soft):
+    """vtb_decode_host on a batch large enough to run in overlapped chunks (H2D of one chunk
+    beside the decode of the previous, a partial last chunk): identical to the device path
+    and to the oracle."""
+    K, L, F = 7, 256, 40961
+    rng = np.random.default_rng(5 + soft)
+    T = L + K - 1
+    x = rng.integers(0, 256, (F, 2 * T if soft else T), dtype=np.uint8)
+    if not soft:
+        x &= 3
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    host = d.decode_host(x)
+    assert (host == dev_decode(d, x)).all()
+    sub = np.r_[0:64, F - 64:F]
+    assert (host[sub] == orc.decode(K, CODES[K], x[sub], L, soft=soft)).all()
+
+
 def test_strided_device_io(orc):
     K, L, F = 7, 640, 300
     unc, rx = random_frames(orc, K, L, F, 0.05, 5)
