@@ -9,6 +9,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -184,10 +185,43 @@ struct DeviceGuard {
     }
 };
 
+// hipGetDeviceProperties costs ~1 ms: answered once per device.
 bool device_is_gfx950(int dev) {
+    static std::mutex mu;
+    static int known[64] = {};  // 0 unknown, 1 gfx950, 2 other / failed
+    if (dev < 0) return false;
+    if (dev < 64) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (known[dev]) return known[dev] == 1;
+    }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
-    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    const bool ok = hipGetDeviceProperties(&prop, dev) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    if (dev < 64) {
+        std::lock_guard<std::mutex> lk(mu);
+        known[dev] = ok ? 1 : 2;
+    }
+    return ok;
+}
+
+// vtb_decode_host_multi's plans, one per (code, input, frame length, device), kept for the
+// process (plan creation, its allocations and the first launch's setup cost milliseconds,
+// against ~0.3 ms for a 4096-frame host batch); vtb_release_cached_plans frees them.
+struct CachedPlan {
+    vtb_code_t code;
+    vtb_input_t input;
+    int32_t L;
+    int device;
+    vtb_plan_t* plan;
+    std::unique_ptr<std::mutex> busy;  // one host thread at a time per plan
+};
+std::mutex g_plan_cache_mu;
+std::vector<CachedPlan> g_plan_cache;
+
+bool same_code(const vtb_code_t& a, const vtb_code_t& b) {
+    if (a.constraint_length != b.constraint_length || a.coded_bits != b.coded_bits) return false;
+    for (int i = 0; i < a.coded_bits && i < 2; i++)
+        if (a.generators[i] != b.generators[i]) return false;
+    return true;
 }
 
 }  // namespace
@@ -447,16 +481,42 @@ int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
         th.emplace_back([&, i, lo, hi]() {
             if (hi <= lo) return;
             vtb_plan_t* p = nullptr;
-            int r = vtb_plan_create(&p, code, input, frame_bits, devs[i]);
-            if (r == VTB_OK) r = vtb_decode_host(p, h_in + lo * ib, h_out + lo * ob, hi - lo);
-            vtb_plan_destroy(p);
-            rc[i] = r;
+            std::mutex* busy = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+                for (CachedPlan& c : g_plan_cache)
+                    if (c.device == devs[i] && c.input == input && c.L == frame_bits && same_code(c.code, *code)) {
+                        p = c.plan;
+                        busy = c.busy.get();
+                        break;
+                    }
+                if (!p) {
+                    int r = vtb_plan_create(&p, code, input, frame_bits, devs[i]);
+                    if (r != VTB_OK) {
+                        rc[i] = r;
+                        return;
+                    }
+                    g_plan_cache.push_back({*code, input, frame_bits, devs[i], p, std::make_unique<std::mutex>()});
+                    busy = g_plan_cache.back().busy.get();
+                }
+            }
+            std::lock_guard<std::mutex> use(*busy);
+            rc[i] = vtb_decode_host(p, h_in + lo * ib, h_out + lo * ob, hi - lo);
         });
     }
     for (auto& t : th) t.join();
     for (int r : rc)
         if (r != VTB_OK) return r;
     return VTB_OK;
+}
+
+void vtb_release_cached_plans(void) {
+    std::lock_guard<std::mutex> lk(g_plan_cache_mu);
+    for (CachedPlan& c : g_plan_cache) {
+        std::lock_guard<std::mutex> use(*c.busy);
+        vtb_plan_destroy(c.plan);
+    }
+    g_plan_cache.clear();
 }
 
 int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t input, size_t streams,

@@ -194,6 +194,11 @@ class ViterbiStream:
         return out, nbits
 
 
+def release_cached_plans():
+    """Free the per-device plans decode_multi keeps between calls (vtb_release_cached_plans)."""
+    native.lib().vtb_release_cached_plans()
+
+
 def decode_multi(frames, code=ConvCode(), frame_bits=1024, soft=False, device_mask=0):
     """Host frames sharded across the GPUs in device_mask (vtb_decode_host_multi)."""
     code = code if isinstance(code, ConvCode) else ConvCode(*code)

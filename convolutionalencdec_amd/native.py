@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "vtb_decode_device",
     "vtb_decode_host",
     "vtb_decode_host_multi",
+    "vtb_release_cached_plans",
     "vtb_decode_frame_legacy",
     "vtb_stream_create",
     "vtb_stream_destroy",
@@ -101,6 +102,8 @@ def lib():
     L.vtb_decode_device.argtypes = [vp, vp, sz, vp, sz, sz, vp]
     L.vtb_decode_host.argtypes = [vp, vp, vp, sz]
     L.vtb_decode_host_multi.argtypes = [cp, ctypes.c_int, i32, vp, vp, sz, ctypes.c_uint32]
+    L.vtb_release_cached_plans.restype = None
+    L.vtb_release_cached_plans.argtypes = []
     L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
     L.vtb_stream_create.argtypes = [ctypes.POINTER(vp), cp, ctypes.c_int, sz, i32, ctypes.c_int]
     L.vtb_stream_destroy.restype = None

@@ -101,8 +101,9 @@ void vtb_plan_destroy(vtb_plan_t* plan);
 /* Decode `frames` frames already resident in device memory, asynchronously on `stream`
  * (a hipStream_t; NULL = default stream).  d_in: frames * in_stride bytes; d_out: frames *
  * out_stride bytes.  Strides >= the per-frame sizes above.  The plan's survivor workspace
- * (8 bytes per frame per trellis step, grown on demand, stream-ordered) is shared by its
- * launches: calls on one plan must use one stream, or the caller orders them. */
+ * (16-64 bytes per trellis step for each wave the device holds at once, grown on demand,
+ * stream-ordered) is shared by its launches: calls on one plan must use one stream, or the
+ * caller orders them. */
 int vtb_decode_device(vtb_plan_t* plan, const uint8_t* d_in, size_t in_stride, uint8_t* d_out,
                       size_t out_stride, size_t frames, void* stream);
 
@@ -112,9 +113,14 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
 
 /* Host buffers sharded across the GPUs in device_mask (bit d = device d; 0 = all visible
  * devices): contiguous frame ranges, one host thread and stream per device, no
- * inter-device traffic (frames are independent). */
+ * inter-device traffic (frames are independent).  The per-device plans (and their device
+ * buffers, sized to the largest shard seen) are created on first use and kept for later
+ * calls with the same code, input kind and frame length. */
 int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,
                           uint8_t* h_out, size_t frames, uint32_t device_mask);
+
+/* Frees the plans vtb_decode_host_multi keeps.  Not concurrently with vtb_decode_host_multi. */
+void vtb_release_cached_plans(void);
 
 /* One hard-input frame of `segments` coded segments from host memory (the legacy
  * VITERBI_DECODER_HARD contract).  Returns the reference's byte count

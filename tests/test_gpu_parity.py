@@ -257,9 +257,22 @@ def test_strided_device_io(orc):
 
 
 def test_multi_device_host_api(orc):
+    """vtb_decode_host_multi: first call (plans created), repeated calls on the kept plans with
+    larger and smaller batches and another code, and after vtb_release_cached_plans."""
+    from convolutionalencdec_amd import release_cached_plans
+
     K, L, F = 7, 256, 1000
     unc, rx = random_frames(orc, K, L, F, 0.04, 8)
-    assert (decode_multi(rx, ConvCode(K, CODES[K]), L) == orc.decode(K, CODES[K], rx, L)).all()
+    ref = orc.decode(K, CODES[K], rx, L)
+    assert (decode_multi(rx, ConvCode(K, CODES[K]), L) == ref).all()
+    assert (decode_multi(rx[:333], ConvCode(K, CODES[K]), L) == ref[:333]).all()
+    big = np.concatenate([rx] * 5)
+    assert (decode_multi(big, ConvCode(K, CODES[K]), L) == np.concatenate([ref] * 5)).all()
+    u9, rx9 = random_frames(orc, 9, L, 300, 0.03, 9)
+    assert (decode_multi(rx9, ConvCode(9, CODES[9]), L) == orc.decode(9, CODES[9], rx9, L)).all()
+    release_cached_plans()
+    assert (decode_multi(rx, ConvCode(K, CODES[K]), L) == ref).all()
+    release_cached_plans()
 
 
 # ---------------- legacy C API (include/viterbiDecoder.h) on the GPU ----------------
