@@ -39,7 +39,7 @@ $(LIB)/libviterbi_legacy_k%.so: $(LEGACY_SRCS) $(LEGACY_HDRS) params/k%/convCode
 	$(CC) $(LEGACY_CFLAGS) -shared -Iparams/k$* -Iinclude -o $@ $(LEGACY_SRCS) params/k$*/convCodeParams.c \
 		-L$(LIB) -lviterbi_amd -Wl,-rpath,'$$ORIGIN'
 
-oracle:
+oracle: legacy
 	$(MAKE) -C oracle
 
 clean:

@@ -641,16 +641,28 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
     if (e != VTB_OK) return e;
     const int32_t L = segments - (code->constraint_length - 1);
     if (L < 1) return VTB_ERR_INVALID;
-    // One cached plan per host thread (the reference API is reentrant per state struct).
+    // One cached plan per host thread (the reference API is reentrant per state struct), with
+    // pinned staging for the frame: the copies are DMA transfers queued behind each other on
+    // the plan's stream with the decode, and one synchronisation ends the call (a synchronous
+    // single-frame call is latency-bound: pageable copies cost ~2x the round trip).
     struct Cache {
         vtb_plan_t* plan = nullptr;
-        ~Cache() { vtb_plan_destroy(plan); }
+        uint8_t* h_in = nullptr;   // pinned, T bytes
+        uint8_t* h_out = nullptr;  // pinned, out_bytes(L)
+        ~Cache() {
+            if (h_in) (void)hipHostFree(h_in);
+            if (h_out) (void)hipHostFree(h_out);
+            vtb_plan_destroy(plan);
+        }
     };
     thread_local Cache cache;
     vtb_plan_t*& p = cache.plan;
     if (!p || p->code.constraint_length != code->constraint_length || p->code.generators[0] != code->generators[0] || p->code.generators[1] != code->generators[1] || p->L != L) {
         vtb_plan_destroy(p);
         p = nullptr;
+        if (cache.h_in) (void)hipHostFree(cache.h_in);
+        if (cache.h_out) (void)hipHostFree(cache.h_out);
+        cache.h_in = cache.h_out = nullptr;
         int dev = 0;
         if (const char* s = std::getenv("VTB_LEGACY_DEVICE")) dev = std::atoi(s);
         int r = vtb_plan_create(&p, code, VTB_INPUT_HARD, L, dev);
@@ -658,9 +670,26 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
             p = nullptr;
             return r;
         }
+        DeviceGuard g(p->device);
+        if (!g.ok || hipHostMalloc(reinterpret_cast<void**>(&cache.h_in), size_t(segments), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&cache.h_out), out_bytes(L), hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(&p->d_in, size_t(segments)) != hipSuccess || hipMalloc(&p->d_out, out_bytes(L)) != hipSuccess ||
+            hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+            return VTB_ERR_NOMEM;  // (the partial cache is released on the next call or at thread exit)
+        p->cap_frames = 1;
     }
-    int r = vtb_decode_host(p, coded, out, 1);
+    DeviceGuard g(p->device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    const size_t ob = out_bytes(L);
+    std::memcpy(cache.h_in, coded, size_t(segments));
+    if (hipMemcpyAsync(p->d_in, cache.h_in, size_t(segments), hipMemcpyHostToDevice, p->stream) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    int r = launch(p, p->d_in, size_t(segments), p->d_out, ob, 1, p->stream);
     if (r != VTB_OK) return r;
+    if (hipMemcpyAsync(cache.h_out, p->d_out, ob, hipMemcpyDeviceToHost, p->stream) != hipSuccess ||
+        hipStreamSynchronize(p->stream) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    std::memcpy(out, cache.h_out, ob);
     return (L - 1) / 8 + 1;  // src/viterbiDecoderButterflyk1.c:256
 }
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# The reference's speedDecode harness, unchanged, on the GPU box (oracle/Makefile `harness`):
+# first built against the reference library (CPU), then against the legacy drop-in
+# (include/viterbiDecoder.h -> libviterbi_legacy_k7 -> GPU, one frame per call).  The harness
+# loops forever printing a rate per second; each run is stopped after a few seconds.  The
+# GPU-using run is the last step of the script.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+secs=${1:-6}
+oracle/_ref/speedDecode_ref > gpurun_out/speedDecode_ref.log 2>&1 &
+pid=$!; sleep $secs; kill $pid; wait $pid 2>/dev/null
+oracle/_ref/speedDecode_amd > gpurun_out/speedDecode_amd.log 2>&1 &
+pid=$!; sleep $((secs + 4)); kill $pid; wait $pid 2>/dev/null
+grep -h "Rate" gpurun_out/speedDecode_ref.log | tail -3 | sed 's/^/ref: /'
+grep -h "Rate" gpurun_out/speedDecode_amd.log | tail -3 | sed 's/^/amd: /'
+exit 0
