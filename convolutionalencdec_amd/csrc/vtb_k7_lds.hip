@@ -315,10 +315,11 @@ __device__ __forceinline__ void put_bits48_global(uint8_t* o, uint64_t bits) {
     o[4] = uint8_t(rh >> 24), o[5] = uint8_t(rh >> 16);
 }
 
-// Two survivor walks of 48 steps each over the global survivor words (the location part of
-// tb_body / tb_body8 only), their loads issued together: the merge test's walks are
-// latency-bound chains of dependent loads, so each lane carries two.
-template <bool SOFT>
+// Two survivor walks of 48 steps each over the survivor words (the location part of tb_body
+// / tb_body8 only), their loads issued together: the merge test's walks are latency-bound
+// chains of dependent loads, so each lane carries two.  G: global words (saddr form at
+// gbase), else LDS words.
+template <bool SOFT, bool G = true>
 __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint32_t& l4b, uint64_t gbase) {
     uint32_t a = cb | l4a, b = cb | l4b;
     if constexpr (SOFT) {
@@ -327,9 +328,14 @@ __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint3
             const int todd = 47 - 2 * j;
             const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
             uint32_t va, vb;
-            asm volatile("global_load_ushort %0, %2, %4 offset:%5\n\tglobal_load_ushort %1, %3, %4 offset:%5\n\t"
-                         "s_waitcnt vmcnt(0)"
-                         : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"((todd >> 4) * 256));
+            if constexpr (G) {
+                asm volatile("global_load_ushort %0, %2, %4 offset:%5\n\tglobal_load_ushort %1, %3, %4 offset:%5\n\t"
+                             "s_waitcnt vmcnt(0)"
+                             : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"((todd >> 4) * 256));
+            } else {
+                asm volatile("ds_read_u16 %0, %2 offset:%4\n\tds_read_u16 %1, %3 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "i"((todd >> 4) * 256));
+            }
             const int pos = 2 + (todd - 1) % 6;
             const uint32_t fa = pos >= sh ? (va << (pos - sh)) : (va >> (sh - pos));
             const uint32_t fb = pos >= sh ? (vb << (pos - sh)) : (vb >> (sh - pos));
@@ -341,9 +347,14 @@ __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint3
         for (int k = 5; k >= 0; k--) {
             const int r0 = (8 * k) % 6;
             uint32_t va, vb;
-            asm volatile("global_load_ubyte %0, %2, %4 offset:%5\n\tglobal_load_ubyte %1, %3, %4 offset:%5\n\t"
-                         "s_waitcnt vmcnt(0)"
-                         : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"(256 * (k >> 1) + (k & 1)));
+            if constexpr (G) {
+                asm volatile("global_load_ubyte %0, %2, %4 offset:%5\n\tglobal_load_ubyte %1, %3, %4 offset:%5\n\t"
+                             "s_waitcnt vmcnt(0)"
+                             : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "s"(gbase), "i"(256 * (k >> 1) + (k & 1)));
+            } else {
+                asm volatile("ds_read_u8 %0, %2 offset:%4\n\tds_read_u8 %1, %3 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(va), "=&v"(vb) : "v"(a), "v"(b), "i"(256 * (k >> 1) + (k & 1)));
+            }
             a = (a & ~0xFCu) | (rotl6c(va & 63u, r0) << 2);
             b = (b & ~0xFCu) | (rotl6c(vb & 63u, r0) << 2);
         }
@@ -365,9 +376,12 @@ __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint3
 // The emission is the frame decoder's verified block-parallel traceback over [e_f, hi_f),
 // 32 blocks per frame, entering at the location known at hi_f.  If the ring no longer holds
 // step e_f (no merge within sa.ring steps) the frame is flagged: -1 bits until last.
-template <bool SOFT>
+// !GS: this call's survivor words [t_begin, t_end) are in LDS at r0 (the walks read them
+// there, older steps from the ring), and afterwards the ones later calls may still walk --
+// from the lower of the two frames' new emission points -- are copied into the ring.
+template <bool SOFT, bool GS>
 __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
-                                 uint64_t gbase, size_t fa, bool has_b, size_t wp) {
+                                 uint64_t gbase, size_t fa, bool has_b, size_t wp, uint32_t r0) {
     const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
     uint32_t* st = sa.state + wp * kStreamStateWords;
     const int e0 = int(st[64 + f]);  // this lane's frame
@@ -375,7 +389,12 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
     const bool real = f == 0 || has_b;
     const bool lost = ((flags0 >> f) & 1u) || t_end - e0 > sa.ring;
     auto colb = [&](int tlo) { return uint32_t(2 * f + 256 * ((tlo % sa.ring) >> 4)); };
+    auto coll = [&](int tlo) { return uint32_t(r0 + 2 * f + 256 * ((tlo - sa.t_begin) >> 4)); };
     auto tb48 = [&](int tlo, uint32_t& l4) -> uint64_t {
+        if (!GS && tlo >= sa.t_begin) {
+            if constexpr (SOFT) return tb_body<false>(coll(tlo), l4, 0);
+            else return tb_body8<false>(coll(tlo), l4, 0);
+        }
         if constexpr (SOFT) return tb_body<true>(colb(tlo), l4, gbase);
         else return tb_body8<true>(colb(tlo), l4, gbase);
     };
@@ -390,7 +409,10 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
         bool walking = !lost && real;
         for (int tlo = t_end - 48; __builtin_amdgcn_readfirstlane(__ballot(walking && tlo >= e0) != 0); tlo -= 48) {
             const bool here = walking && tlo >= e0;
-            if (here) tb_walk48_pair<SOFT>(colb(tlo), la, lb, gbase);
+            if (here) {
+                if (!GS && tlo >= sa.t_begin) tb_walk48_pair<SOFT, false>(coll(tlo), la, lb, 0);
+                else tb_walk48_pair<SOFT, true>(colb(tlo), la, lb, gbase);
+            }
             const uint32_t ref = __shfl(la, 32 * f);
             const uint64_t same = __ballot(la == ref && lb == ref);
             const bool merged = uint32_t(same >> (32 * f)) == 0xFFFFFFFFu;
@@ -448,8 +470,21 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
     // new emission state; the streams restart after last
     const uint64_t lostmask = __ballot(lost && real && blk == 0);
     const uint32_t flags = sa.last ? 0u : uint32_t((lostmask & 1u) | ((lostmask >> 32) & 1u) << 1);
-    if (blk == 0) st[64 + f] = uint32_t(sa.last || lost ? (sa.last ? 0 : e0) : hi);
+    const int e_next = sa.last || lost ? (sa.last ? 0 : e0) : hi;
+    if (blk == 0) st[64 + f] = uint32_t(e_next);
     if (lane == 0) st[66] = flags;
+    if (!GS && !sa.last) {
+        // survivor columns later calls may walk: [max(t_begin, min_f e_next), t_end), 16 steps
+        // (one 256-B column of both frames' words) per wave store
+        const int eb = has_b ? __shfl(e_next, 32) : __shfl(e_next, 0);
+        int lo = min(__shfl(e_next, 0), eb);
+        lo = max(lo, sa.t_begin) & ~15;
+        extern __shared__ uint4 smem4[];
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(smem4) + r0);
+        uint32_t* ring = reinterpret_cast<uint32_t*>(gbase);
+        for (int t = lo; t < t_end; t += 16)
+            ring[((t % sa.ring) >> 4) * 64 + lane] = words[((t - sa.t_begin) >> 4) * 64 + lane];
+    }
 }
 
 // GS = false: survivor words in LDS at [r0, r0 + 16 Tpad).  GS = true: survivor words in a
@@ -500,7 +535,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
                                         const StreamArgs& sa, size_t wp, size_t slot, bool pre, size_t next,
                                         uint32_t& pra, uint32_t& prb, const uint32_t (&off)[6]) {
-    static_assert(GS || !STREAM, "the streaming decoder keeps its survivors in a global ring");
+
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
     using H = Hist<SOFT>;
@@ -512,7 +547,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     if (dbg & 16) return;  // measurement only: launch cost
     const size_t fa = wp * 2, fb = fa + 1;
     const bool has_b = fb < frames;
-    const uint64_t gbase = GS ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
+    const uint64_t gbase = (GS || STREAM) ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
     const uint8_t* inA = in + fa * in_stride;
     const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
 
@@ -645,7 +680,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
-        uint32_t* dchunk = dec + (t0 >> 4) * 64 + widx;
+        uint32_t* dchunk = dec + (((STREAM && !GS) ? t0 - tbeg : t0) >> 4) * 64 + widx;  // (stream: this call's words)
         // GS: byte offset of the lane's words (streaming: position in the survivor ring)
         const uint32_t gvo = 4u * (((STREAM ? t0 % sa.ring : t0) >> 4) * 64 + widx);
 
@@ -734,7 +769,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     __syncthreads();
     if constexpr (STREAM) {
         if (!sa.last) sa.state[wp * kStreamStateWords + lane] = M;
-        stream_traceback<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp);
+        stream_traceback<SOFT, GS>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, uint32_t(r0));
         return;
     }
     if (LOOP && !GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
@@ -913,11 +948,19 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s) {
     if (a.frames == 0) return hipSuccess;
     if (!a.ws || !s.state || !s.out_bits || s.ring < 48 || s.ring % 48 || s.t_begin % 48 || s.t_end % 48)
         return hipErrorInvalidValue;
-    auto kern = a.soft ? k7_lds_kernel<true, true, true, false> : k7_lds_kernel<false, true, true, false>;
-    const size_t lds = (kRingBytes + 255) / 256 * 256;
+    // This call's survivor words in LDS (16 B per step) while 8 waves per CU still fit (calls
+    // up to ~1,000 segments): the merge test and the emission then walk LDS except for the
+    // steps carried over from earlier calls; longer calls keep every word in the ring.
+    const size_t r0 = (kRingBytes + 255) / 256 * 256;
+    const size_t lds_l = r0 + 16 * size_t(s.t_end - s.t_begin);
+    const bool in_lds = lds_l <= (160 * 1024) / 8 && !(debug_flags() & 64);  // VTB_DEBUG bit 6: ring only
+    auto kern = in_lds ? (a.soft ? k7_lds_kernel<true, false, true, false> : k7_lds_kernel<false, false, true, false>)
+                       : (a.soft ? k7_lds_kernel<true, true, true, false> : k7_lds_kernel<false, true, true, false>);
+    const size_t lds = in_lds ? lds_l : r0;
     const size_t waves = (a.frames + 1) / 2;
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, s.t_end, 0, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring), s);
+                       a.T, a.L, s.t_end, 0, int(r0), a.frames, 0, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring),
+                       s);
     return hipGetLastError();
 }
 

@@ -90,6 +90,28 @@ def test_random_chunking_matches_whole_frame(orc, soft, L, F):
         assert (counts[:-1] % 8 == 0).all() and (counts >= 0).all()
 
 
+@pytest.mark.parametrize("soft", [False, True])
+def test_mixed_call_lengths_match_whole_frame(orc, soft):
+    """Calls short enough to keep their survivor words in LDS (copied into the ring only
+    from the new emission point) mixed with calls that keep every word in the ring, on noisy
+    frames (slow survivor merges carry unmerged steps across calls), also with no merge
+    inside short calls (pure noise)."""
+    rng = np.random.default_rng(77 + soft)
+    L, F = 12000, 7
+    for p, sigma in ((0.06, 0.65), (0.5, 4.0)):
+        if soft:
+            unc, xh = random_frames(orc, K, L, F, 0.0, 9 + int(10 * sigma), soft=True, sigma=sigma)
+        else:
+            unc, xh = random_frames(orc, K, L, F, p, 9 + int(100 * p))
+        sb = 2 if soft else 1
+        x = torch.from_numpy(np.ascontiguousarray(xh).reshape(F, -1)).cuda()
+        vs = ViterbiStream(CODE, streams=F, soft=soft)
+        want = expect_bits(orc, xh, L, soft)
+        got, counts = push_frame(vs, x, sb, random_chunks(rng, L + K - 1, sizes=(5, 48, 400, 1000, 1100, 3000)))
+        for f in range(F):
+            assert got[f].size == L and (got[f] == want[f]).all(), (p, f)
+
+
 def test_golden_vectors_streamed(orc):
     """The reference's golden frames (hard and the soft bridge q = 255*bit) pushed in 100-segment chunks."""
     for key, L, unc, rx, dec in golden_sets(K):
