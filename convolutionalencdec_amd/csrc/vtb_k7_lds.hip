@@ -173,8 +173,9 @@ __host__ __device__ __forceinline__ uint32_t rev6(uint32_t l) {
 // and each window is one read, one shift and one bit-field insert on the address.
 // Returns the 48 decoded bits with bit 0 = step tlo (a sextet's bits are its end location
 // in l' numbering, oldest step at bit 0).
+// One dependent read per window.
 template <bool GS>
-__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t gbase) {
+__device__ __forceinline__ uint64_t tb_body_serial(uint32_t cb, uint32_t& l4, uint64_t gbase) {
     uint32_t a = cb | l4;
     uint64_t bits = 0;
 #pragma unroll
@@ -195,6 +196,67 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t 
     }
     l4 = a & 0xFCu;
     return bits;
+}
+
+// Two windows per dependent read: window j's two decisions are the only address bits in
+// which window j+1's word can differ, so the read of window j and the four candidate words
+// of window j+1 (one base address with those bits clear, the bits as immediate offsets) are
+// issued together, and window j's bits then pick window j+1's word.
+template <bool GS>
+__device__ __forceinline__ uint64_t tb_body_spec(uint32_t cb, uint32_t& l4, uint64_t gbase) {
+    uint32_t a = cb | l4;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 24; j += 2) {
+        const int todd = 47 - 2 * j, todd1 = todd - 2;  // odd steps of windows j, j+1 (relative to tlo)
+        const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+        const int wi1 = (todd1 & 15) >> 1, sh1 = 8 * (wi1 & 1) + 2 * (wi1 >> 1);
+        const int pos = 2 + (todd - 1) % 6, pos1 = 2 + (todd1 - 1) % 6;  // address bits of the decisions
+        if (j % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - j / 3));
+        const uint32_t base = a & ~(3u << pos);  // window j+1's word address without window j's bits
+        const int o = (todd >> 4) * 256, o1 = (todd1 >> 4) * 256, d = 1 << pos;
+        uint32_t v, c0, c1, c2, c3;
+        if constexpr (GS) {
+            asm volatile(
+                "global_load_ushort %0, %5, %7 offset:%8\n\t"
+                "global_load_ushort %1, %6, %7 offset:%9\n\tglobal_load_ushort %2, %6, %7 offset:%10\n\t"
+                "global_load_ushort %3, %6, %7 offset:%11\n\tglobal_load_ushort %4, %6, %7 offset:%12\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(v), "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+                : "v"(a), "v"(base), "s"(gbase), "i"(o), "i"(o1), "i"(o1 + d), "i"(o1 + 2 * d), "i"(o1 + 3 * d));
+        } else {
+            asm volatile(
+                "ds_read_u16 %0, %5 offset:%7\n\t"
+                "ds_read_u16 %1, %6 offset:%8\n\tds_read_u16 %2, %6 offset:%9\n\t"
+                "ds_read_u16 %3, %6 offset:%10\n\tds_read_u16 %4, %6 offset:%11\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(v), "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+                : "v"(a), "v"(base), "i"(o), "i"(o1), "i"(o1 + d), "i"(o1 + 2 * d), "i"(o1 + 3 * d));
+        }
+        const uint32_t f = (v >> sh) & 3u;  // window j's decisions = address bits pos, pos + 1
+        a = base | (f << pos);
+        if ((j + 1) % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - (j + 1) / 3));
+        const uint32_t lo = (f & 1u) ? c1 : c0, hi = (f & 1u) ? c3 : c2;
+        const uint32_t v1 = (f & 2u) ? hi : lo;
+        a = (a & ~(3u << pos1)) | (((v1 >> sh1) & 3u) << pos1);
+    }
+    l4 = a & 0xFCu;
+    return bits;
+}
+
+// The serial form is the shipped one.  The speculative form (VTB_EXP_TBSPEC, measurement
+// only) measured slower where it matters: LDS words 6 % per 4,096-frame launch (2.5 random
+// reads per window cost more LDS bandwidth than the latency they hide, with 8 waves per CU
+// tracing back at once), global words 2 % slower on config C3 (65,536 x 2,048 bits: the
+// extra loads queue behind other waves' traffic), 2 % faster only for one 4,096-frame round
+// with global words.
+template <bool GS>
+__device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t gbase) {
+#if defined(VTB_EXP_TBSPEC)
+    return tb_body_spec<GS>(cb, l4, gbase);
+#else
+    return tb_body_serial<GS>(cb, l4, gbase);
+#endif
 }
 
 __device__ __forceinline__ uint32_t rotl6c(uint32_t x, int r) { return r == 0 ? x : ((x << r) | (x >> (6 - r))) & 63u; }

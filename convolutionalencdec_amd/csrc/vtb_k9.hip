@@ -168,6 +168,35 @@ __device__ __forceinline__ uint32_t lprime_of(uint32_t a) { return (a & 0xFCu) |
 __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t gbase) {
     uint32_t a = cb | la;
     uint64_t bits = 0;
+#ifdef VTB_EXP_TBSPEC
+    // Measurement only (1 % slower per 4,096-frame soft launch): two windows per dependent
+    // load, as vtb_k7_lds.hip tb_body_spec.
+#pragma unroll
+    for (int j = 0; j < 24; j += 2) {
+        const int todd = 47 - 2 * j, todd1 = todd - 2;
+        if (j % 4 == 0) bits |= uint64_t(lprime_of(a)) << (8 * (5 - j / 4));  // octet ending at tlo + todd + 1
+        const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+        const int wi1 = (todd1 & 15) >> 1, sh1 = 8 * (wi1 & 1) + 2 * (wi1 >> 1);
+        const int pos = addr_pos((todd - 1) & 7), pos1 = addr_pos((todd1 - 1) & 7);
+        const uint32_t base = a & ~(3u << pos);
+        const int o = (todd >> 4) * kColBytes, o1 = (todd1 >> 4) * kColBytes, d = 1 << pos;
+        uint32_t v, c0, c1, c2, c3;
+        asm volatile(
+            "global_load_ushort %0, %5, %7 offset:%8\n\t"
+            "global_load_ushort %1, %6, %7 offset:%9\n\tglobal_load_ushort %2, %6, %7 offset:%10\n\t"
+            "global_load_ushort %3, %6, %7 offset:%11\n\tglobal_load_ushort %4, %6, %7 offset:%12\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(v), "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+            : "v"(a), "v"(base), "s"(gbase), "i"(o), "i"(o1), "i"(o1 + d), "i"(o1 + 2 * d), "i"(o1 + 3 * d));
+        const uint32_t f = (v >> sh) & 3u;
+        a = base | (f << pos);
+        const uint32_t lo = (f & 1u) ? c1 : c0, hi = (f & 1u) ? c3 : c2;
+        const uint32_t v1 = (f & 2u) ? hi : lo;
+        a = (a & ~(3u << pos1)) | (((v1 >> sh1) & 3u) << pos1);
+    }
+    la = a & 0x3FCu;
+    return bits;
+#endif
 #pragma unroll
     for (int j = 0; j < 24; j++) {
         const int todd = 47 - 2 * j;

@@ -24,6 +24,7 @@ for v in "$@"; do
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
     base) build base ;;
+    tbspec) build tbspec -DVTB_EXP_TBSPEC ;;
     nonop) build nonop -DVTB_EXP_NONOP ;;
     bitop3) build bitop3 -DVTB_EXP_BITOP3 ;;
     rd1) build rd1 -DVTB_EXP_RD1 ;;
