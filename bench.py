@@ -96,6 +96,17 @@ class Timer:
         return self.allreduce_max(dt)
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return None
+
+
 def cpu_baseline(seconds, threads, frame_bits):
     """Reference decoder (oracle/_ref/libref_k7.so, compiled from the reference sources) on
     this host: the speedDecode protocol (speedDecode.c:37-116) with the workload's frame
@@ -117,10 +128,12 @@ def cpu_baseline(seconds, threads, frame_bits):
         os.dup2(2, 1)
         try:
             mbps = lib.ref_speed(seconds, threads, pkt_bytes)
+            one = lib.ref_speed(min(2.0, seconds), 1, pkt_bytes)  # also one core
         finally:
             os.dup2(saved, 1)
             os.close(saved)
         return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
+                "single_core_value": round(one, 2), "cpu_model": cpu_model(),
                 "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
                           f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "
                           f"{seconds:g} s, one decoder state per thread"}
