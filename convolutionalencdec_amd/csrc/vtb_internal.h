@@ -31,7 +31,7 @@ struct Launch {
 // Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
 // kernel: bit 2 skip traceback verification, bit 3 warm-up walk only, bit 4 return at entry, bit 5
 // one wave per frame pair instead of the persistent grid, bit 6 streaming survivors in the
-// global ring only).  Never
+// global ring only, bit 8 never split frames across the halves of a wave).  Never
 // set in production; outputs are garbage when set.
 inline int debug_flags() {
     const char* v = getenv("VTB_DEBUG");

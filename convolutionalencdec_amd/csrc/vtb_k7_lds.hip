@@ -105,6 +105,13 @@ int tb_block(int T) {
     return (per + 47) / 48 * 48;
 }
 int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
+// SPLIT: frame A's half ends at t1 (a multiple of 48), frame B's starts kSplitWarm steps
+// earlier, and both run t1 steps: t1 = the smallest multiple of 48 with 2 t1 - kSplitWarm >= T.
+// kSplitWarm = 96: frame B's metrics then equal frame A's up to a constant at t1 in all of
+// 2,000 simulated soft frames at SNR -5 dB (48: 98.2 %, and every miss costs its wave a
+// second, unsplit pass).
+constexpr int kSplitWarm = 96;
+__host__ __device__ constexpr int split_t1(int T) { return ((T + kSplitWarm) / 2 + kChunk - 1) / kChunk * kChunk; }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
 int region0(int T) {  // multiple of 256: the traceback edits survivor-word addresses in place
@@ -591,7 +598,7 @@ __device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, s
 // decodes after this one (its chunk 0 is prefetched into (pra, prb) before the traceback;
 // LDS variant only, whose traceback issues no global loads that would wait behind it).
 
-template <bool SOFT, bool GS, bool STREAM, bool LOOP>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT>
 __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
@@ -607,11 +614,20 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t* dec = reinterpret_cast<uint32_t*>(smem + r0);
     const int lane = threadIdx.x;
     if (dbg & 16) return;  // measurement only: launch cost
-    const size_t fa = wp * 2, fb = fa + 1;
-    const bool has_b = fb < frames;
+    // SPLIT: one frame per wave, its two halves in the u16 halves of the registers: A = steps
+    // [0, t1), B = steps [t1 - 96, T) (96 warm-up steps from equal start metrics).  If B's
+    // metrics at t1 equal A's up to a constant, B's decisions from t1 on are the frame's
+    // (the trellis only compares differences); otherwise the wave decodes the frame again
+    // the normal way (pass 1).  Per-pass values:
+    const int t1s = SPLIT ? split_t1(T) : 0;
+    bool sp = SPLIT;                            // this pass runs split
+    int Tb = SPLIT ? T - t1s + kSplitWarm : T;  // frame B's steps (local)
+    const size_t fa = SPLIT ? wp : wp * 2, fb = fa + 1;
+    const bool has_b = !SPLIT && fb < frames;
     const uint64_t gbase = (GS || STREAM) ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
     const uint8_t* inA = in + fa * in_stride;
-    const uint8_t* inB = in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
+    const uint8_t* inB = SPLIT ? inA + (SOFT ? 2 : 1) * size_t(t1s - kSplitWarm)
+                               : in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
 
     // Table staging: lane r < 48 builds the row of step 48c + r from the raw input bytes of
     // that step (soft q0 | q1 << 8, hard the byte).  The loads are issued in asm at the start
@@ -619,7 +635,8 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // their wait up) and waited for where the chunk is staged, 36+ steps later.
     const int srow = lane < kChunk ? lane : lane - kChunk;  // staging row (lanes 48-63 duplicate 0-15)
     // (wave-uniform frame bases in SGPRs, one 32-bit lane offset)
-    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA)), baseB = uniform64(reinterpret_cast<uint64_t>(inB));
+    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA));
+    uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(inB));
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         const int t = c * kChunk + srow;
         const uint32_t tc = uint32_t(t < T ? t : T - 1);
@@ -637,6 +654,16 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             } else {
                 asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
                              : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            }
+        } else if constexpr (SPLIT) {
+            constexpr uint32_t SB = SOFT ? 2 : 1;
+            const uint32_t tcb = uint32_t(t < Tb ? t : Tb - 1);
+            if constexpr (SOFT) {
+                asm volatile("global_load_ushort %0, %2, %4\n\tglobal_load_ushort %1, %3, %5"
+                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tc), "v"(SB * tcb), "s"(baseA), "s"(baseB));
+            } else {
+                asm volatile("global_load_ubyte %0, %2, %4\n\tglobal_load_ubyte %1, %3, %5"
+                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tc), "v"(SB * tcb), "s"(baseA), "s"(baseB));
             }
         } else if constexpr (SOFT) {
             asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
@@ -692,7 +719,18 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
 #undef VTB_W2
-        if (PADCHK && (c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows
+        if (SPLIT && sp) {
+            // split pass: padding rows of frame B only (step >= Tb); frame A's half is real
+            if (PADCHK && c * kChunk + srow >= Tb) {
+                constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1, LO = 0xFFFFu, HI = 0xFFFF0000u;
+                const uint32_t tie = et[0] - e[0];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    col[k * kCol] = make_uint2(e[k] & LO, (et[3 - k] & LO) | ((PADW + tie) & HI));
+                    col[(4 + k) * kCol] = make_uint2((et[k] & LO) | (tie & HI), (e[3 - k] & LO) | (PADW & HI));
+                }
+            }
+        } else if (PADCHK && (c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows
             constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
@@ -708,7 +746,16 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         stage_write(c, e, et, std::true_type{});
     };
 
+    for (int pass = 0; pass < (SPLIT ? 2 : 1); pass++) {
+    if (SPLIT && pass == 1) {  // the split halves did not converge: the frame the normal way
+        sp = false;
+        Tb = T;
+        baseB = baseA;
+        __syncthreads();
+    }
     uint32_t M = (lane == 0) ? H::BIAS * kR1 : (H::BIAS + H::SC * INIT) * kR1;
+    if (SPLIT && sp) M = (M & 0xFFFFu) | (H::BIAS << 16);  // frame B's half: equal start metrics
+    uint32_t msave = 0;                                      // (SPLIT) frame B's metrics at t1
     // first step of this launch: 0, or (streaming) where the previous call stopped
     const int tbeg = STREAM ? sa.t_begin : 0;
     if constexpr (STREAM) {
@@ -734,7 +781,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
-    const int tacs = (dbg & 2) ? 0 : Tpad;
+    const int tacs = (dbg & 2) ? 0 : (SPLIT && sp ? t1s : Tpad);
     // One 48-step chunk of the ACS (fully unrolled); PADTAG: this chunk stages the chunk that
     // holds step T (padding rows possible).
     auto acs_chunk = [&](const int t0, auto padtag) __attribute__((always_inline)) {
@@ -816,7 +863,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #undef VTB_RENORM_APPLY
 #undef VTB_RD
     };
-    {
+    if constexpr (SPLIT) {
+        for (int t0 = 0; t0 < tacs; t0 += kChunk) {
+            acs_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
+            if (t0 == kSplitWarm - kChunk) msave = M;
+        }
+    } else {
         // chunks in order; only the one before the last stages padding rows
         const int tstage = tacs - 2 * kChunk;  // the chunk that stages the last one
         int t0 = tbeg;
@@ -835,17 +887,32 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         return;
     }
     if (LOOP && !GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
+    if (SPLIT && sp) {
+        // frame A's metrics at t1 against frame B's at its step 96 (= t1), histories masked:
+        // equal up to a constant -> B's decisions from t1 on are the frame's
+        constexpr uint32_t KEEP = 0xFFFFu & ~(H::SC - 1);
+        const uint32_t a = M & KEEP, b = (msave >> 16) & KEEP;
+        const uint32_t a0 = __builtin_amdgcn_readfirstlane(a), b0 = __builtin_amdgcn_readfirstlane(b);
+        if (__ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) != ~0ull) continue;
+    }
     if (dbg & 1) return;
 
     // ---------------- traceback: verified block-parallel chains ----------------
     const int f = lane >> 5, blk = lane & 31;
     const uint32_t cb0 = uint32_t((GS ? 0 : r0) + 2 * f);  // this frame's 16-bit half of the word columns
     uint8_t* ob = tab + f * 4 * tbb;                                      // decoded bytes, index t/8
-    const int top = (blk + 1) * tbb;
+    // (SPLIT pass: 48-step blocks over [0, t1) per half; frame A's last block (lane nA - 1)
+    // enters at frame B's location at its step 96 (lane 34's exit), frame B's blocks 0 and 1
+    // are warm-up only)
+    const int tbp = (SPLIT && sp) ? kChunk : tbb, nA = t1s / kChunk;
+    const int top = (blk + 1) * tbp;
     const int start_full = top + kTbWarm;
-    const int start = min(start_full, Tpad);
-    const bool known = start >= T;  // walk starts on the known path (location 0 at and past T)
-    const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;  // dbg bit 3: warm-up walk only
+    const int start = min(start_full, (SPLIT && sp) ? t1s : Tpad);
+    // walk starts on the known path (location 0 at and past T)
+    constexpr int kB0 = 32 + kSplitWarm / kChunk;  // frame B's first decoded block (lane)
+    const bool known = (SPLIT && sp) ? (f == 1 && start >= Tb) || (f == 0 && blk >= nA) || (f == 1 && lane < kB0)
+                                     : start >= T;
+    const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbp) / 48;  // dbg bit 3: warm-up walk only
     auto tb48 = [&](uint32_t cb, uint32_t& l4) {
         if constexpr (SOFT) return tb_body<GS>(cb, l4, gbase);
         else return tb_body8<GS>(cb, l4, gbase);
@@ -867,12 +934,20 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t fin = loc;  // survivor's location at step blk * tbb
     bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement only): skip verification
     for (int round = 0; round < 33; round++) {
-        const uint32_t sf = __shfl_down(fin, 1);  // lane 31 (frame A's last block) is known
+        // successor's exit (lane 31, frame A's last block, is known)
+        const uint32_t sf = (SPLIT && sp) ? __shfl(fin, lane == nA - 1 ? kB0 : (lane + 1) & 63) : __shfl_down(fin, 1);
         const bool ok = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
-        const uint32_t badf = uint32_t(bad >> (32 * f));       // this frame's failed blocks
-        const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+        bool succ_proven;
+        if (SPLIT && sp) {  // one chain: frame A's blocks 0..nA-1, then frame B's blocks 2..31
+            const uint64_t cm = (bad & ((uint64_t(1) << nA) - 1)) | ((bad >> kB0) << nA);
+            const int pos = f == 0 ? blk : nA + lane - kB0;
+            succ_proven = (cm >> (pos + 1)) == 0;
+        } else {
+            const uint32_t badf = uint32_t(bad >> (32 * f));  // this frame's failed blocks
+            succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+        }
         if (!ok && succ_proven) {
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
@@ -888,7 +963,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // copy the decoded bytes out (bits past L are zero: the survivor ends in state 0)
     const int nbytes = (L + 7) >> 3;
     const bool words = ((nbytes | out_stride | (size_t)out) & 3) == 0;  // wave-uniform
-    if (words) {  // lanes 0-31 copy frame A, 32-63 frame B, one dword each per pass
+    if (SPLIT && sp) {  // frame A's half up to t1, then frame B's from its step 96
+        uint8_t* o = out + fa * out_stride;
+        const int na = t1s >> 3;
+        for (int i = lane; i < nbytes; i += 64) o[i] = i < na ? tab[i] : tab[4 * tbb + kSplitWarm / 8 + (i - na)];
+    } else if (words) {  // lanes 0-31 copy frame A, 32-63 frame B, one dword each per pass
         uint8_t* o = out + (f ? fb : fa) * out_stride;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tab + f * 4 * tbb);
         if (f == 0 || has_b)
@@ -904,6 +983,8 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // the prefetched registers are complete before they leave this function (no copy of an
     // in-flight load destination can happen past here)
     if (LOOP && !GS && next < (frames + 1) / 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+    break;
+    }
 }
 
 // LOOP: persistent over frame pairs, wave b decodes pairs b, b + grid, ... (the grid is what
@@ -911,22 +992,23 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // the dispatcher refilling freed slots unevenly).  !LOOP: one wave per pair, for batches the
 // CUs hold in one round and for the streaming decoder (the loop's extra live state costs
 // ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
-template <bool SOFT, bool GS, bool STREAM, bool LOOP>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false>
 __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
                                                     uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
     static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
+    static_assert(!SPLIT || (!GS && !STREAM && !LOOP), "split frames: LDS survivors, one round");
     const size_t pairs = (frames + 1) / 2;
     uint32_t pra = 0, prb = 0;  // next pair's chunk-0 input, prefetched during the traceback (LDS variant)
     uint32_t off[6];
     column_offsets(table, off);
     if constexpr (!LOOP) {
-        k7_pair<SOFT, GS, STREAM, false>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
+        k7_pair<SOFT, GS, STREAM, false, SPLIT>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
                                          ws_wave, sa, blockIdx.x, blockIdx.x, false, pairs, pra, prb, off);
     } else {
         for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
-            k7_pair<SOFT, GS, STREAM, true>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
+            k7_pair<SOFT, GS, STREAM, true, false>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
                                             ws_wave, sa, wp, blockIdx.x, !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb,
                                             off);
             __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
@@ -942,9 +1024,9 @@ constexpr size_t kMaxWsBytes = size_t(1) << 30;  // survivor workspace cap (glob
 template <bool GS>
 size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T) : lds_bytes(a.T); }
 
-template <bool GS, bool LOOP = true>
+template <bool GS, bool LOOP = true, bool SPLIT = false>
 auto kernel_of(const Launch& a) {
-    return a.soft ? k7_lds_kernel<true, GS, false, LOOP> : k7_lds_kernel<false, GS, false, LOOP>;
+    return a.soft ? k7_lds_kernel<true, GS, false, LOOP, SPLIT> : k7_lds_kernel<false, GS, false, LOOP, SPLIT>;
 }
 
 // Persistent grid: the frame pairs, at most what the CUs hold at once (occupancy of this
@@ -977,8 +1059,19 @@ hipError_t launch_k7(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (GS && !a.ws) return hipErrorInvalidValue;
     const size_t lds = lds_of<GS>(a);
-    const size_t grid = grid_waves<GS>(a);
+    size_t grid = grid_waves<GS>(a);
     auto kern = grid < (a.frames + 1) / 2 ? kernel_of<GS, true>(a) : kernel_of<GS, false>(a);
+    // Batches the CUs hold at one frame per wave (up to 2 per SIMD at L = 1024) run split
+    // (one frame per wave, both halves at once: k7_pair SPLIT): twice the waves, about half
+    // the dependent steps per wave.  VTB_DEBUG bit 8 (measurement only): never split.
+    if (!GS && a.T >= 240 && split_t1(a.T) <= 32 * kChunk && !(debug_flags() & 256)) {
+        auto ks = kernel_of<false, false, true>(a);
+        const int per_cu = resident_per_cu(reinterpret_cast<const void*>(ks), lds);
+        if (per_cu > 0 && a.frames <= size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1)) {
+            kern = ks;
+            grid = a.frames;
+        }
+    }
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
