@@ -101,6 +101,26 @@ def test_soft_random_vs_oracle(orc, K, L, kernel):
 
 
 @pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("L", [234, 235, 500, 1519, 2970])
+def test_split_frames_vs_oracle(orc, L, soft):
+    """Small K=7 batches decode each frame in one wave as two halves at once (DESIGN.md 4.1,
+    split frames): the frame-length limits of that mode (T = 240, t1 = 1536), clean, noisy and
+    pure-noise frames (the halves' metrics then rarely converge: the unsplit re-decode), an
+    odd count, and one frame alone -- against the oracle."""
+    K = 7
+    code = ConvCode(K, CODES[K])
+    d = ViterbiDecoder(code, frame_bits=L, soft=soft)
+    for noise, seed in ((0.0, 1), (0.05, 2), (0.5, 3)):
+        if soft:
+            unc, x = random_frames(orc, K, L, 65, 0.0, 50 + seed + L, soft=True, sigma=(0.3, 0.63, 4.0)[seed - 1])
+        else:
+            unc, x = random_frames(orc, K, L, 65, noise, 50 + seed + L)
+        want = orc.decode(K, CODES[K], x, L, soft=soft)
+        assert (dev_decode(d, x) == want).all(), (L, soft, seed)
+        assert (dev_decode(d, x[:1]) == want[:1]).all(), (L, soft, seed)
+
+
+@pytest.mark.parametrize("soft", [False, True])
 @pytest.mark.parametrize("K,L,F", [(7, 1024, 12289), (7, 1024, 40961), (9, 512, 20481)])
 def test_persistent_grid_many_pairs_per_wave(orc, K, L, F, soft, kernel):
     """Batches with several frame pairs per wave of the persistent grid (more pairs than the
