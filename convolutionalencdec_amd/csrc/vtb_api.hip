@@ -684,11 +684,13 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
     std::memcpy(cache.h_in, coded, size_t(segments));
     if (hipMemcpyAsync(p->d_in, cache.h_in, size_t(segments), hipMemcpyHostToDevice, p->stream) != hipSuccess)
         return VTB_ERR_DEVICE;
-    int r = launch(p, p->d_in, size_t(segments), p->d_out, ob, 1, p->stream);
+    // the kernel writes the decoded bytes straight into the pinned host buffer (no D2H copy;
+    // visible to the host once the stream has synchronised)
+    uint8_t* d_out = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out), cache.h_out, 0) != hipSuccess) return VTB_ERR_DEVICE;
+    int r = launch(p, p->d_in, size_t(segments), d_out, ob, 1, p->stream);
     if (r != VTB_OK) return r;
-    if (hipMemcpyAsync(cache.h_out, p->d_out, ob, hipMemcpyDeviceToHost, p->stream) != hipSuccess ||
-        hipStreamSynchronize(p->stream) != hipSuccess)
-        return VTB_ERR_DEVICE;
+    if (hipStreamSynchronize(p->stream) != hipSuccess) return VTB_ERR_DEVICE;
     std::memcpy(out, cache.h_out, ob);
     return (L - 1) / 8 + 1;  // src/viterbiDecoderButterflyk1.c:256
 }
