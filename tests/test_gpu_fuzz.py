@@ -1,0 +1,80 @@
+"""GPU: seeded random sweep over the decoder's code paths -- K (generic path K=3/5, K=7 LDS /
+global-survivor / persistent / split-frame kernels, K=9), frame length, batch size (odd counts,
+single frames, batches past one launch round), hard and soft input, clean to pure-noise
+channels, device and strided buffers -- each case against the oracle, bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import CODES, Oracle, random_frames
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, ViterbiDecoder, native  # noqa: E402
+
+THREADS = min(16, os.cpu_count() or 1)
+K3 = (0b111, 0b101)
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+def _cases(n=128, seed=20261016):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        K = int(rng.choice([3, 5, 7, 7, 7, 7, 9, 9]))
+        L = int(rng.choice([1, 8, 57, 200, 234, 500, 1024, 1519, 2048, 3000, 4100]))
+        if K == 9 and L > 2048:
+            L = 2048
+        if K in (3, 5) and L > 2048:
+            L = 1024
+        F = int(rng.choice([1, 2, 3, 65, 257, 1000, 2049, 4097, 9001]))
+        while F * L > 12_000_000 or (K == 9 and F * L > 3_000_000):
+            F = max(1, F // 3)
+        soft = bool(rng.integers(0, 2))
+        noise = float(rng.choice([0.0, 0.03, 0.07, 0.5]))
+        strided = bool(rng.integers(0, 4) == 0)
+        out.append((i, K, L, F, soft, noise, strided))
+    return out
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: f"{c[0]}-K{c[1]}-L{c[2]}-F{c[3]}-{'soft' if c[4] else 'hard'}")
+def test_random_case_vs_oracle(orc, case):
+    i, K, L, F, soft, noise, strided = case
+    g = K3 if K == 3 else CODES[K]
+    if soft:
+        sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
+        unc, x = random_frames(orc, K, L, F, 0.0, 1000 + i, soft=True, sigma=sigma, g=g)
+    else:
+        unc, x = random_frames(orc, K, L, F, noise, 1000 + i, g=g)
+    x = np.ascontiguousarray(x).reshape(F, -1)
+    want = orc.decode(K, g, x, L, soft=soft, threads=THREADS)
+    d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
+    if strided:  # rows inside wider device buffers, output rows wider than the frame
+        pad_in, pad_out = 37, 5
+        xi = torch.zeros((F, x.shape[1] + pad_in), dtype=torch.uint8, device="cuda")
+        xi[:, :x.shape[1]] = torch.from_numpy(x).cuda()
+        ob = (L + 7) // 8
+        out = torch.full((F, ob + pad_out), 0xA5, dtype=torch.uint8, device="cuda")
+        native.check(native.lib().vtb_decode_device(d._plan, xi.data_ptr(), xi.stride(0), out.data_ptr(), out.stride(0),
+                                                    F, None), "vtb_decode_device")
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert (got[:, ob:] == 0xA5).all(), "wrote past the output row"
+        got = got[:, :ob]
+    else:
+        got = d.decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (case, bad.size, bad[:8])
