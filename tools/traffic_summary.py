@@ -24,7 +24,8 @@ repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def mean_counter(d, name):
     vals = []
     for r in csv.DictReader(open(os.path.join(root, d, "run_counter_collection.csv"))):
-        if r["Counter_Name"] == name and "kernel" in r["Kernel_Name"]:
+        # the decoder's dispatches only (not the device frame generator's or runtime copies)
+        if r["Counter_Name"] == name and any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
             vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals), len(vals)
 
