@@ -4,7 +4,8 @@ C ABI:      include/viterbi_amd.h            -> lib/libviterbi_amd.so (HIP, gfx9
 Legacy API: include/viterbiDecoder.h, convEncode.h -> lib/libviterbi_legacy_k<K>.so
 Python:     plumbing over the C ABI (native.py, decoder.py).
 """
-from .decoder import K7_CODE, K9_CODE, ConvCode, ViterbiDecoder, ViterbiStream, decode_multi, release_cached_plans  # noqa: F401,E501
+from .decoder import (K7_CODE, K9_CODE, ConvCode, GenKDecoder, ViterbiDecoder, ViterbiStream, decode_multi,  # noqa: F401
+                      release_cached_plans)
 from .native import LIB_DIR, LIB_PATH, VtbError  # noqa: F401
 
 __all__ = ["ConvCode", "ViterbiDecoder", "ViterbiStream", "decode_multi", "release_cached_plans", "K7_CODE", "K9_CODE", "VtbError", "LIB_DIR", "LIB_PATH"]

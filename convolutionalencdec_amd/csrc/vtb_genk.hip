@@ -1,0 +1,164 @@
+// General rate-k/n decoder (k input bits per trellis step).
+//
+// The reference's generic decoder (src/viterbiDecoder.c:52-234) defines the trellis: state =
+// the last S = K-1 input segments (k bits each, newest in the low bits); destination d has
+// 2^k predecessors src = d / 2^k + e * 2^((S-1)k) (:101-110), the edge label is the encoder
+// output for delay (src << k) | (d mod 2^k) (:32-49 with convEncode.c:19-44, 132-161), the
+// branch metric the Hamming distance to the received segment (:85-90), the survivor the
+// first minimum (argmin2/4/8 with <=, convHelpers.h:40-63).  Its 5K-step register-exchange
+// traceback in uint8 registers (:119-229) loses bits for k*5K > 8, so this decoder is
+// terminated maximum likelihood with a full traceback from state 0 instead, exact int32
+// metrics and the reference's start metrics 0 / (uint8)(N+1) (:236-262); the checker is
+// oracle_genk_decode, and k = 1 reproduces the k=1 decoder bit for bit.
+//
+// One wave64 per frame.  The N = 2^(kS) <= 256 states spread over the lanes (state d in
+// lane d % 64, register d / 64); metrics double-buffered in LDS (each lane gathers its 2^k
+// predecessors with ds_read), decisions as k ballot words per register per step in LDS,
+// edge labels from an LDS table of the N * 2^k delays.  A completeness kernel: these codes
+// are not on the headline path, so it favours generality over the K=7 kernel's tricks.
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "viterbi_amd.h"
+#include "vtb_internal.h"
+
+namespace vtb {
+namespace {
+
+int gen_status() { return hipGetLastError() == hipSuccess ? VTB_OK : VTB_ERR_DEVICE; }
+
+uint32_t gen_rev(uint64_t v, int bits) {  // convEncode.c:163-174
+    uint32_t r = 0;
+    for (int i = 0; i < bits; i++) r = (r << 1) | uint32_t((v >> i) & 1u);
+    return r;
+}
+
+struct GenArgs {
+    int k, S, n, N, T, L, R;
+    uint32_t rg[8];  // generators bit-reversed over k*K bits (convEncode.c:163-174)
+};
+
+struct GenLayout {  // LDS byte offsets
+    size_t tab, met, inb, outb, dec, total;
+};
+
+GenLayout gen_layout(int N, int E, int T, int L, int R, int k) {
+    GenLayout l;
+    l.dec = 0;                                       // T * R * k u64 words
+    l.met = l.dec + 8 * size_t(T) * R * k;           // 2 * N int32
+    l.tab = l.met + 8 * size_t(N);                   // N * E bytes
+    l.inb = (l.tab + size_t(N) * E + 15) & ~size_t(15);  // T bytes
+    l.outb = (l.inb + size_t(T) + 15) & ~size_t(15);     // L / 8 bytes
+    l.total = (l.outb + size_t(L / 8) + 15) & ~size_t(15);
+    return l;
+}
+
+__global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                  uint8_t* __restrict__ out, size_t out_stride, size_t frames,
+                                                  GenArgs a, GenLayout ly) {
+    extern __shared__ uint64_t gsm[];
+    uint8_t* sm = reinterpret_cast<uint8_t*>(gsm);
+    uint64_t* dec = reinterpret_cast<uint64_t*>(sm + ly.dec);
+    int32_t* met = reinterpret_cast<int32_t*>(sm + ly.met);
+    uint8_t* tab = sm + ly.tab;
+    uint8_t* inb = sm + ly.inb;
+    uint8_t* outb = sm + ly.outb;
+    const int lane = threadIdx.x;
+    const size_t f = blockIdx.x;
+    if (f >= frames) return;
+    const int k = a.k, N = a.N, E = 1 << k, kS = k * a.S, T = a.T, R = a.R;
+    const uint32_t nmask = (1u << a.n) - 1u;
+
+    for (int i = lane; i < N * E; i += 64) {  // edge labels, index = delay (src << k) | bits
+        uint32_t o = 0;
+        for (int j = 0; j < a.n; j++) o |= (uint32_t(__popc(uint32_t(i) & a.rg[j])) & 1u) << j;
+        tab[i] = uint8_t(o);
+    }
+    const uint8_t* row = in + f * in_stride;
+    for (int i = lane; i < T; i += 64) inb[i] = row[i];
+    for (int i = lane; i < a.L / 8; i += 64) outb[i] = 0;
+    const int32_t init = int32_t(uint8_t(N + 1));
+    for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
+    __syncthreads();
+
+    int cur = 0;
+    for (int t = 0; t < T; t++) {
+        const uint32_t rx = inb[t];
+        const int32_t* mc = met + cur * N;
+        int32_t* mn = met + (cur ^ 1) * N;
+        for (int r = 0; r < R; r++) {
+            const int d = r * 64 + lane;
+            int be = 0;
+            if (d < N) {
+                const int bits = d & (E - 1);
+                int32_t best = 0;
+                for (int e = 0; e < E; e++) {
+                    const int src = (d >> k) | (e << (kS - k));
+                    const int32_t pm = mc[src] + int32_t(__popc((uint32_t(tab[(src << k) | bits]) ^ rx) & nmask));
+                    if (e == 0 || pm < best) best = pm, be = e;  // first minimum
+                }
+                mn[d] = best;
+            }
+            for (int j = 0; j < k; j++) {
+                const uint64_t w = __ballot((be >> j) & 1);
+                if (lane == 0) dec[(size_t(t) * R + r) * k + j] = w;
+            }
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+
+    if (lane == 0) {  // traceback from state 0 (terminated frame)
+        int s = 0;
+        for (int t = T - 1; t >= 0; t--) {
+            if (t < T - a.S) {
+                const int seg = s & (E - 1);
+                for (int j = 0; j < k; j++) {
+                    const int pos = t * k + j;
+                    if ((seg >> (k - 1 - j)) & 1) outb[pos >> 3] |= uint8_t(0x80u >> (pos & 7));
+                }
+            }
+            const uint64_t* w = dec + (size_t(t) * R + (s >> 6)) * k;
+            int e = 0;
+            for (int j = 0; j < k; j++) e |= int((w[j] >> (s & 63)) & 1u) << j;
+            s = (s >> k) | (e << (kS - k));
+        }
+    }
+    __syncthreads();
+    uint8_t* orow = out + f * out_stride;
+    for (int i = lane; i < a.L / 8; i += 64) orow[i] = outb[i];
+}
+
+}  // namespace
+}  // namespace vtb
+
+extern "C" {
+
+int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const uint8_t* d_in, size_t in_stride,
+                           uint8_t* d_out, size_t out_stride, size_t frames, void* stream) {
+    if (!code || !d_in || !d_out) return VTB_ERR_INVALID;
+    const int k = code->input_bits, K = code->constraint_length, n = code->coded_bits;
+    if (k < 1 || K < 2 || n < 1 || n > 8) return VTB_ERR_INVALID;
+    const int S = K - 1;
+    if (k * S > 8 || k * K > 12) return VTB_ERR_UNSUPPORTED;  // N <= 256 states, N * 2^k <= 4096 labels
+    for (int i = 0; i < n; i++)
+        if (code->generators[i] == 0 || (code->generators[i] >> (k * K))) return VTB_ERR_INVALID;
+    if (info_bits < 8 || info_bits % 8 || info_bits % k) return VTB_ERR_INVALID;
+    const int T = info_bits / k + S, N = 1 << (k * S), E = 1 << k, R = (N + 63) / 64;
+    if (in_stride < size_t(T) || out_stride < size_t(info_bits / 8)) return VTB_ERR_INVALID;
+    if (frames == 0) return VTB_OK;
+    vtb::GenArgs a{};
+    a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R;
+    for (int i = 0; i < n; i++) a.rg[i] = vtb::gen_rev(code->generators[i], k * K);
+    const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, R, k);
+    if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
+    if (ly.total > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(vtb::genk_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, int(ly.total)) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    hipLaunchKernelGGL(vtb::genk_kernel, dim3(unsigned(frames)), dim3(64), ly.total, (hipStream_t)stream, d_in,
+                       in_stride, d_out, out_stride, frames, a, ly);
+    return vtb::gen_status();
+}
+
+}  // extern "C"

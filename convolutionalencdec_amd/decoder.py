@@ -213,3 +213,41 @@ def decode_multi(frames, code=ConvCode(), frame_bits=1024, soft=False, device_ma
                                            out.ctypes.data_as(ctypes.c_void_p), x.shape[0], device_mask),
         "vtb_decode_host_multi")
     return out
+
+
+class GenKDecoder:
+    """Hard-decision decoder for a rate-k/n code (k input bits per trellis step), the
+    reference's generic `viterbiDecoderHard` (src/viterbiDecoder.c:52-234) as terminated
+    maximum likelihood on the GPU (vtb_genk_decode_device).  `generators` over k*K bits,
+    MSB = newest input bit (src/convEncode.c conventions)."""
+
+    def __init__(self, k, K, generators, info_bits):
+        if info_bits % 8 or info_bits % k:
+            raise ValueError("info_bits must be a multiple of 8 and of k (viterbiDecoder.c:222-227)")
+        self.k, self.K, self.generators, self.info_bits = int(k), int(K), tuple(int(g) for g in generators), int(info_bits)
+        self._code = native.VtbGenKCode.make(k, K, self.generators)
+        self.in_bytes = info_bits // k + K - 1
+        self.out_bytes = info_bits // 8
+
+    def decode_device(self, frames, out=None, stream=None):
+        """frames: torch uint8 tensor on a ROCm device, rows of in_bytes coded segments."""
+        import torch
+
+        if frames.dtype != torch.uint8 or not frames.is_cuda:
+            raise TypeError("decode_device expects a torch.uint8 tensor on a ROCm device")
+        x = frames.reshape(frames.shape[0], -1)
+        if x.shape[1] != self.in_bytes or x.stride(1) != 1:
+            raise ValueError(f"expected rows of {self.in_bytes} contiguous bytes, got {tuple(x.shape)}")
+        F = x.shape[0]
+        if out is None:
+            out = torch.empty((F, self.out_bytes), dtype=torch.uint8, device=frames.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        with torch.cuda.device(frames.device):
+            native.check(
+                native.lib().vtb_genk_decode_device(ctypes.byref(self._code), self.info_bits,
+                                                    ctypes.c_void_p(x.data_ptr()), x.stride(0),
+                                                    ctypes.c_void_p(out.data_ptr()), out.stride(0), F,
+                                                    ctypes.c_void_p(stream)),
+                "vtb_genk_decode_device")
+        return out

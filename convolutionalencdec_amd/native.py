@@ -48,7 +48,27 @@ EXPORTED_SYMBOLS = (
     "vtb_channel_device",
     "vtb_awgn_kq",
     "vtb_bsc_p32",
+    "vtb_genk_decode_device",
 )
+
+
+class VtbGenKCode(ctypes.Structure):
+    """vtb_genk_code_t: a rate-k/n code (include/viterbi_amd.h)."""
+    _fields_ = [
+        ("input_bits", ctypes.c_int32),
+        ("constraint_length", ctypes.c_int32),
+        ("coded_bits", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("generators", ctypes.c_uint64 * 8),
+    ]
+
+    @classmethod
+    def make(cls, k, K, g):
+        c = cls()
+        c.input_bits, c.constraint_length, c.coded_bits = int(k), int(K), len(g)
+        for i, v in enumerate(g):
+            c.generators[i] = int(v)
+        return c
 
 
 class VtbCode(ctypes.Structure):
@@ -122,10 +142,11 @@ def lib():
     L.vtb_awgn_kq.argtypes = [ctypes.c_double]
     L.vtb_bsc_p32.restype = ctypes.c_uint32
     L.vtb_bsc_p32.argtypes = [ctypes.c_double]
+    L.vtb_genk_decode_device.argtypes = [ctypes.POINTER(VtbGenKCode), i32, vp, sz, vp, sz, sz, vp]
     for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
                  "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_stream_create", "vtb_stream_decode",
                  "vtb_device_count", "vtb_payload_device",
-                 "vtb_encode_device", "vtb_channel_device"):
+                 "vtb_encode_device", "vtb_channel_device", "vtb_genk_decode_device"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

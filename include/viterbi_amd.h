@@ -207,6 +207,30 @@ int vtb_channel_device(vtb_input_t output, double param, uint64_t seed, const ui
 int64_t vtb_awgn_kq(double snr_db);
 uint32_t vtb_bsc_p32(double p);
 
+/* ---- General rate-k/n codes (k input bits per trellis step) ----
+ * Replaces the reference's generic decoder viterbiDecoderHard (src/viterbiDecoder.c:52-234,
+ * src/viterbiDecoder.h:160), whose register-exchange traceback in uint8 registers drops
+ * bits for k > 1; this one is terminated maximum likelihood over the same trellis (see
+ * csrc/vtb_genk.hip).  The code uses the reference encoder's conventions
+ * (src/convEncode.c:19-174): k bits per segment shifted in MSB-first, generators over k*K
+ * bits (MSB = newest input bit), coded bit i of a segment = generator i, S = K-1 zero
+ * segments of termination. */
+typedef struct {
+    int32_t input_bits;        /* k, 1..4 */
+    int32_t constraint_length; /* K in k-bit segments; k*(K-1) <= 8 and k*K <= 12 */
+    int32_t coded_bits;        /* n, 1..8 */
+    int32_t reserved;          /* 0 */
+    uint64_t generators[8];    /* g[0..n-1], each nonzero and below 2^(k*K) */
+} vtb_genk_code_t;
+
+/* Hard-decision decode of `frames` rows of info_bits/k + K-1 coded segment bytes (row stride
+ * in_stride) into rows of info_bits/8 bytes, MSB-first (out_stride); info_bits a multiple of
+ * 8 and of k (the reference's own requirement, viterbiDecoder.c:222-227).  Device pointers,
+ * asynchronous on `stream` (a hipStream_t, 0 = default) of the current device.
+ * VTB_ERR_UNSUPPORTED when the trellis or the frame exceeds one CU's LDS. */
+int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const uint8_t* d_in, size_t in_stride,
+                           uint8_t* d_out, size_t out_stride, size_t frames, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

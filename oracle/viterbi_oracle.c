@@ -409,3 +409,86 @@ uint32_t oracle_bsc_p32(double p) {
     if (p >= 1.0) return 0xFFFFFFFFu;
     return (uint32_t)floor(p * 4294967296.0);
 }
+
+/* ---- general rate-k/n codes (header: oracle_genk_*) ---- */
+
+static uint64_t genk_rev(uint64_t g, int bits) { /* convEncode.c:163-174 */
+    uint64_t r = 0;
+    for (int i = 0; i < bits; i++) r = (r << 1) | ((g >> i) & 1u);
+    return r;
+}
+
+static uint8_t genk_out(int n, const uint64_t* rg, uint64_t delay) { /* convEncode.c:132-161 */
+    uint8_t o = 0;
+    for (int i = 0; i < n; i++) o |= (uint8_t)(parity64(delay & rg[i]) << i);
+    return o;
+}
+
+int oracle_genk_encode(int k, int K, int n, const uint64_t* g, const uint8_t* uncoded, int nbytes, uint8_t* coded) {
+    if (k < 1 || K < 2 || n < 1 || n > 8 || k * K > 64 || (nbytes * 8) % k) return -1;
+    uint64_t rg[8];
+    for (int i = 0; i < n; i++) rg[i] = genk_rev(g[i], k * K);
+    uint64_t delay = 0;
+    int seg = 0, pos = 0;
+    for (int c = 0; c < nbytes * 8 / k; c++) { /* convEncode.c:55-97 */
+        for (int j = 0; j < k; j++, pos++) delay = (delay << 1) | ((uncoded[pos >> 3] >> (7 - (pos & 7))) & 1u);
+        coded[seg++] = genk_out(n, rg, delay);
+    }
+    for (int i = 0; i < K - 1; i++) { /* :99-122, termination */
+        delay <<= k;
+        coded[seg++] = genk_out(n, rg, delay);
+    }
+    return seg;
+}
+
+int oracle_genk_decode(int k, int K, int n, const uint64_t* g, const uint8_t* coded, int info_bits, uint8_t* out) {
+    const int S = K - 1, kS = k * S;
+    if (k < 1 || K < 2 || n < 1 || n > 8 || kS > 16 || info_bits < 8 || info_bits % 8 || info_bits % k) return -1;
+    const int N = 1 << kS, E = 1 << k, T = info_bits / k + S;
+    uint64_t rg[8];
+    for (int i = 0; i < n; i++) rg[i] = genk_rev(g[i], k * K);
+    int32_t* m = malloc(sizeof(int32_t) * 2 * (size_t)N);
+    uint8_t* dec = malloc((size_t)T * N);
+    if (!m || !dec) {
+        free(m);
+        free(dec);
+        return -1;
+    }
+    int32_t *cur = m, *nxt = m + N;
+    for (int s = 0; s < N; s++) cur[s] = s == 0 ? 0 : (int32_t)(uint8_t)(N + 1);
+    for (int t = 0; t < T; t++) {
+        const uint8_t rx = coded[t];
+        for (int d = 0; d < N; d++) {
+            const int bits = d & (E - 1);
+            int32_t best = 0;
+            int be = 0;
+            for (int e = 0; e < E; e++) {
+                const int src = (d >> k) | (e << (kS - k));
+                const uint64_t delay = ((uint64_t)src << k) | (uint64_t)bits;
+                const int32_t pm = cur[src] + __builtin_popcount((unsigned)(genk_out(n, rg, delay) ^ rx) & ((1u << n) - 1));
+                if (e == 0 || pm < best) best = pm, be = e; /* first minimum */
+            }
+            nxt[d] = best;
+            dec[(size_t)t * N + d] = (uint8_t)be;
+        }
+        int32_t* x = cur;
+        cur = nxt;
+        nxt = x;
+    }
+    const int nb = info_bits / 8;
+    memset(out, 0, (size_t)nb);
+    int s = 0;
+    for (int t = T - 1; t >= 0; t--) {
+        if (t < T - S) {
+            const int seg = s & (E - 1);
+            for (int j = 0; j < k; j++) {
+                const int pos = t * k + j;
+                if ((seg >> (k - 1 - j)) & 1) out[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
+            }
+        }
+        s = (s >> k) | ((int)dec[(size_t)t * N + s] << (kS - k));
+    }
+    free(m);
+    free(dec);
+    return nb;
+}

@@ -33,6 +33,8 @@ class Oracle:
         L.oracle_config_check.argtypes = [i, v]
         L.oracle_edge_table.argtypes = [i, v, v]
         L.oracle_encode.argtypes = [i, v, v, i, v]
+        L.oracle_genk_encode.argtypes = [i, i, i, v, v, i, v]
+        L.oracle_genk_decode.argtypes = [i, i, i, v, v, i, v]
         L.oracle_decode_hard.argtypes = [i, v, v, i, v]
         L.oracle_decode_soft.argtypes = [i, v, v, i, v]
         L.oracle_decode_batch.argtypes = [i, v, i, v, sz, i, v, sz, sz, i]
@@ -108,6 +110,31 @@ class Oracle:
             row = np.ascontiguousarray(unc[f])
             o = np.zeros(T, np.uint8)
             assert self.L.oracle_encode(K, G, vp(row), nb, vp(o)) == T
+            out[f] = o
+        return out
+
+    def genk_encode(self, k, K, g, uncoded):
+        """Rows of payload bytes -> rows of info_bits/k + K-1 coded segments (oracle_genk_encode)."""
+        unc = np.ascontiguousarray(uncoded, np.uint8)
+        F, nb = unc.shape
+        T = 8 * nb // k + K - 1
+        G = (ctypes.c_uint64 * 8)(*[int(v) for v in g])
+        out = np.zeros((F, T), np.uint8)
+        for f in range(F):
+            row = np.ascontiguousarray(unc[f])
+            o = np.zeros(T, np.uint8)
+            assert self.L.oracle_genk_encode(k, K, len(g), G, vp(row), nb, vp(o)) == T
+            out[f] = o
+        return out
+
+    def genk_decode(self, k, K, g, frames, info_bits):
+        x = np.ascontiguousarray(frames, np.uint8)
+        G = (ctypes.c_uint64 * 8)(*[int(v) for v in g])
+        out = np.zeros((x.shape[0], info_bits // 8), np.uint8)
+        for f in range(x.shape[0]):
+            row = np.ascontiguousarray(x[f])
+            o = np.zeros(info_bits // 8, np.uint8)
+            assert self.L.oracle_genk_decode(k, K, len(g), G, vp(row), info_bits, vp(o)) == info_bits // 8
             out[f] = o
         return out
 
@@ -221,3 +248,28 @@ def hard_to_soft(rx):
     """Map hard segments to the soft format's hard-equivalent input q = 255*bit."""
     rx = np.asarray(rx, np.uint8)
     return np.stack([(rx & 1) * 255, ((rx >> 1) & 1) * 255], axis=-1).astype(np.uint8)
+
+
+# General rate-k/n codes (k, K, generators over k*K bits) for the general-k decoder
+# (SURVEY.md 8 f4).  The first two are params/k4_k2n3 and params/k3_k3n4, whose reference
+# encoder oracle/Makefile builds (oracle/_ref/librefenc_*.so).
+GENK_CODES = (
+    (2, 4, (0xB5, 0x6B, 0xD9)),
+    (3, 3, (0x1ED, 0x15B, 0x0B7, 0x1A7)),
+    (4, 3, (0xB5D, 0x6E3, 0x9A7, 0xF19, 0x5CB)),
+    (2, 5, (0x2DB, 0x1B5, 0x3A7)),
+    (1, 7, (0o113, 0o171)),
+)
+GENK_REF_PARAMS = {"k4_k2n3": GENK_CODES[0], "k3_k3n4": GENK_CODES[1]}
+
+
+def genk_frames(orc, k, K, g, info_bits, F, p, seed):
+    """Random payloads, encoded by the oracle, each coded bit flipped with probability p."""
+    rng = np.random.default_rng(seed)
+    unc = rng.integers(0, 256, (F, info_bits // 8), dtype=np.uint8)
+    coded = orc.genk_encode(k, K, g, unc)
+    n = len(g)
+    flips = np.zeros(coded.shape, np.uint8)
+    for i in range(n):
+        flips |= ((rng.random(coded.shape) < p).astype(np.uint8) << i)
+    return unc, coded ^ flips

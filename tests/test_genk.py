@@ -1,0 +1,105 @@
+"""General rate-k/n codes, CPU side: the checker's encoder against the
+reference's own encoder compiled for k = 2 and k = 3 (oracle/_ref/librefenc_*.so), the
+checker's decoder against noise-free round trips, against the k = 1 checker (which the
+reference's golden vectors pin) and against a pure-Python restatement; the C ABI's argument
+checks (no GPU call)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from helpers import CODES, GENK_CODES, GENK_REF_PARAMS, REF_DIR, Oracle, genk_frames, random_frames, vp
+
+from convolutionalencdec_amd import native
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.mark.parametrize("name", sorted(GENK_REF_PARAMS))
+def test_genk_encoder_matches_reference_encoder(orc, name):
+    path = os.path.join(REF_DIR, f"librefenc_{name}.so")
+    if not os.path.exists(path):
+        pytest.skip("reference encoder not built (oracle/Makefile ref)")
+    ref = ctypes.CDLL(path)
+    k, K, g = GENK_REF_PARAMS[name]
+    assert (ref.refenc_k(), ref.refenc_K(), ref.refenc_n()) == (k, K, len(g))
+    rng = np.random.default_rng(7)
+    for nb in (3, 6, 48, 384):
+        unc = rng.integers(0, 256, nb, dtype=np.uint8)
+        T = nb * 8 // k + K - 1
+        want = np.zeros(T + 8, np.uint8)
+        assert ref.refenc_encode(vp(unc), nb, vp(want)) == T
+        got = orc.genk_encode(k, K, g, unc[None])[0]
+        assert (got == want[:T]).all(), (name, nb)
+
+
+@pytest.mark.parametrize("code", GENK_CODES, ids=lambda c: f"k{c[0]}K{c[1]}n{len(c[2])}")
+def test_genk_round_trip(orc, code):
+    k, K, g = code
+    L = 96 if k == 3 else 256
+    unc, coded = genk_frames(orc, k, K, g, L, 6, 0.0, 11)
+    assert (orc.genk_decode(k, K, g, coded, L) == unc).all()
+
+
+@pytest.mark.parametrize("K", [7, 9])
+def test_genk_k1_equals_k1_decoder(orc, K):
+    """k = 1: same trellis, start metrics and tie rule as the k=1 decoder (the reference's
+    golden vectors pin that one), so every noisy frame decodes identically."""
+    L = 512
+    unc, x = random_frames(orc, K, L, 12, 0.06, 5 + K)
+    want = orc.decode(K, CODES[K], x, L)
+    assert (orc.genk_decode(1, K, CODES[K], x, L) == want).all()
+    assert (orc.genk_encode(1, K, CODES[K], unc) == orc.encode(K, CODES[K], unc)).all()
+
+
+def _py_genk_decode(k, K, g, coded, L):
+    """Pure-Python restatement (small cases only) of the terminated decode."""
+    S, n = K - 1, len(g)
+    N, E = 1 << (k * S), 1 << k
+    rg = [int(format(v, f"0{k * K}b")[::-1], 2) for v in g]
+    lab = lambda delay: sum((bin(delay & rg[i]).count("1") & 1) << i for i in range(n))
+    m = [0] + [(N + 1) & 0xFF] * (N - 1)
+    dec = []
+    for rx in coded:
+        nm, dd = [0] * N, [0] * N
+        for d in range(N):
+            c = [m[(d >> k) | (e << (k * S - k))] + bin(lab((((d >> k) | (e << (k * S - k))) << k) | (d & (E - 1))) ^ int(rx)).count("1") for e in range(E)]
+            dd[d] = c.index(min(c))
+            nm[d] = c[dd[d]]
+        m = nm
+        dec.append(dd)
+    T = len(coded)
+    bits = [0] * L
+    s = 0
+    for t in range(T - 1, -1, -1):
+        if t < T - S:
+            for j in range(k):
+                bits[t * k + j] = (s >> (k - 1 - j)) & 1
+        s = (s >> k) | (dec[t][s] << (k * S - k))
+    return np.packbits(np.array(bits, np.uint8))
+
+
+@pytest.mark.parametrize("code", GENK_CODES[:2], ids=lambda c: f"k{c[0]}K{c[1]}")
+def test_genk_oracle_vs_python(orc, code):
+    k, K, g = code
+    L = 48
+    unc, coded = genk_frames(orc, k, K, g, L, 3, 0.15, 3)
+    got = orc.genk_decode(k, K, g, coded, L)
+    for f in range(3):
+        assert (got[f] == _py_genk_decode(k, K, g, coded[f], L)).all()
+
+
+def test_genk_abi_argument_checks():
+    lib = native.lib()
+    buf = ctypes.create_string_buffer(4096)
+    c = native.VtbGenKCode.make(2, 4, (0xB5, 0x6B, 0xD9))
+    call = lambda code, L, ins=600, outs=128: lib.vtb_genk_decode_device(ctypes.byref(code), L, buf, ins, buf, outs, 1, None)
+    assert call(c, 1020) == native.VTB_ERR_INVALID          # not a multiple of 8
+    assert call(c, 1024, ins=100) == native.VTB_ERR_INVALID  # input row too short
+    assert call(native.VtbGenKCode.make(2, 4, (0x1B5, 1, 1)), 1024) == native.VTB_ERR_INVALID  # generator > 2^(kK)
+    assert call(native.VtbGenKCode.make(3, 4, (0x1B5, 1, 1)), 1032) == native.VTB_ERR_UNSUPPORTED  # 512 states
+    assert lib.vtb_genk_decode_device(ctypes.byref(c), 1024, buf, 600, buf, 128, 0, None) == native.VTB_OK

@@ -1,0 +1,79 @@
+"""GPU: the general rate-k/n decoder (vtb_genk_decode_device) against the
+checker's oracle_genk_decode on noisy frames, bit for bit; k = 1 against the k=1 batch
+decoder (pinned by the reference's golden vectors); strided rows."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import CODES, GENK_CODES, Oracle, genk_frames, golden_sets
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, GenKDecoder, ViterbiDecoder, native  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+@pytest.mark.parametrize("code", GENK_CODES, ids=lambda c: f"k{c[0]}K{c[1]}n{len(c[2])}")
+@pytest.mark.parametrize("L,F,p", [(48, 7, 0.1), (1032, 300, 0.04), (2040, 65, 0.0)])
+def test_genk_gpu_vs_oracle(orc, code, L, F, p):
+    k, K, g = code
+    unc, coded = genk_frames(orc, k, K, g, L, F, p, L + F + k)
+    want = orc.genk_decode(k, K, g, coded, L)
+    d = GenKDecoder(k, K, g, L)
+    got = d.decode_device(torch.from_numpy(coded).cuda()).cpu().numpy()
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (code, L, bad.size, bad[:8])
+    if p == 0.0:
+        assert (got == unc).all()  # noise-free frames decode to their payload
+
+
+def test_genk_gpu_k1_golden_vectors():
+    """k = 1, K = 7: the reference's own golden frames decode to the reference's output."""
+    for key, L, unc, rx, dec in golden_sets(7):
+        if L % 8:
+            continue
+        d = GenKDecoder(1, 7, CODES[7], L)
+        got = d.decode_device(torch.from_numpy(np.ascontiguousarray(rx)).cuda()).cpu().numpy()
+        assert (got == dec).all(), key
+
+
+def test_genk_gpu_k1_equals_batch_decoder(orc):
+    from helpers import random_frames
+
+    L = 1024
+    unc, x = random_frames(orc, 7, L, 200, 0.06, 99)
+    xt = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    a = GenKDecoder(1, 7, CODES[7], L).decode_device(xt).cpu().numpy()
+    b = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L).decode_device(xt).cpu().numpy()
+    assert (a == b).all()
+
+
+def test_genk_gpu_strided_rows(orc):
+    k, K, g = GENK_CODES[0]
+    L, F = 512, 33
+    unc, coded = genk_frames(orc, k, K, g, L, F, 0.05, 4)
+    T = coded.shape[1]
+    xi = torch.zeros((F, T + 29), dtype=torch.uint8, device="cuda")
+    xi[:, :T] = torch.from_numpy(coded).cuda()
+    out = torch.full((F, L // 8 + 7), 0xA5, dtype=torch.uint8, device="cuda")
+    code = native.VtbGenKCode.make(k, K, g)
+    native.check(native.lib().vtb_genk_decode_device(ctypes.byref(code), L, ctypes.c_void_p(xi.data_ptr()), xi.stride(0),
+                                                     ctypes.c_void_p(out.data_ptr()), out.stride(0), F, None),
+                 "vtb_genk_decode_device")
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert (got[:, L // 8:] == 0xA5).all()
+    assert (got[:, :L // 8] == orc.genk_decode(k, K, g, coded, L)).all()
