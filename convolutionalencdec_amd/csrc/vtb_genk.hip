@@ -18,6 +18,7 @@
 // are not on the headline path, so it favours generality over the K=7 kernel's tricks.
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include "viterbi_amd.h"
 #include "vtb_internal.h"
@@ -42,10 +43,10 @@ struct GenLayout {  // LDS byte offsets
     size_t tab, met, inb, outb, dec, total;
 };
 
-GenLayout gen_layout(int N, int E, int T, int L, int R, int k) {
+GenLayout gen_layout(int N, int E, int T, int L, int R, int k, bool gdec) {
     GenLayout l;
-    l.dec = 0;                                       // T * R * k u64 words
-    l.met = l.dec + 8 * size_t(T) * R * k;           // 2 * N int32
+    l.dec = 0;                                             // T * R * k u64 words (in LDS unless gdec)
+    l.met = l.dec + (gdec ? 0 : 8 * size_t(T) * R * k);   // 2 * N int32
     l.tab = l.met + 8 * size_t(N);                   // N * E bytes
     l.inb = (l.tab + size_t(N) * E + 15) & ~size_t(15);  // T bytes
     l.outb = (l.inb + size_t(T) + 15) & ~size_t(15);     // L / 8 bytes
@@ -53,12 +54,15 @@ GenLayout gen_layout(int N, int E, int T, int L, int R, int k) {
     return l;
 }
 
+// GDEC: decision words in a global workspace (one slot per frame of the launch) instead of
+// LDS, for trellises whose words would hold the CU to one or two waves.
+template <bool GDEC>
 __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                   uint8_t* __restrict__ out, size_t out_stride, size_t frames,
-                                                  GenArgs a, GenLayout ly) {
+                                                  GenArgs a, GenLayout ly, uint64_t* __restrict__ ws) {
     extern __shared__ uint64_t gsm[];
     uint8_t* sm = reinterpret_cast<uint8_t*>(gsm);
-    uint64_t* dec = reinterpret_cast<uint64_t*>(sm + ly.dec);
+    uint64_t* dec = GDEC ? ws + size_t(blockIdx.x) * size_t(a.T) * a.R * a.k : reinterpret_cast<uint64_t*>(sm + ly.dec);
     int32_t* met = reinterpret_cast<int32_t*>(sm + ly.met);
     uint8_t* tab = sm + ly.tab;
     uint8_t* inb = sm + ly.inb;
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
             }
             for (int j = 0; j < k; j++) {
                 const uint64_t w = __ballot((be >> j) & 1);
-                if (lane == 0) dec[(size_t(t) * R + r) * k + j] = w;
+                if (lane == j) dec[(size_t(t) * R + r) * k + j] = w;
             }
         }
         cur ^= 1;
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         }
     }
     __syncthreads();
-    uint8_t* orow = out + f * out_stride;
+    uint8_t* orow = out + f * out_stride;  // (GDEC: lane 0 read its own stores back)
     for (int i = lane; i < a.L / 8; i += 64) orow[i] = outb[i];
 }
 
@@ -150,15 +154,35 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     vtb::GenArgs a{};
     a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R;
     for (int i = 0; i < n; i++) a.rg[i] = vtb::gen_rev(code->generators[i], k * K);
-    const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, R, k);
+    // decision words in LDS while they leave room for 4 waves per CU, else in a workspace
+    const size_t dec_bytes = 8 * size_t(T) * R * k;
+    const bool gdec = dec_bytes > 32 * 1024;
+    const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, R, k, gdec);
     if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
-    if (ly.total > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(vtb::genk_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, int(ly.total)) != hipSuccess)
-        return VTB_ERR_DEVICE;
-    hipLaunchKernelGGL(vtb::genk_kernel, dim3(unsigned(frames)), dim3(64), ly.total, (hipStream_t)stream, d_in,
-                       in_stride, d_out, out_stride, frames, a, ly);
-    return vtb::gen_status();
+    hipStream_t st = (hipStream_t)stream;
+    if (!gdec) {
+        if (ly.total > 64 * 1024 &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(vtb::genk_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(ly.total)) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        hipLaunchKernelGGL(vtb::genk_kernel<false>, dim3(unsigned(frames)), dim3(64), ly.total, st, d_in, in_stride,
+                           d_out, out_stride, frames, a, ly, nullptr);
+        return vtb::gen_status();
+    }
+    // workspace from the stream's pool, up to 1 GiB per launch (frames in launches of that)
+    const size_t per = std::max<size_t>(1, (size_t(1) << 30) / dec_bytes);
+    const size_t chunk = std::min(frames, per);
+    void* ws = nullptr;
+    if (hipMallocAsync(&ws, chunk * dec_bytes, st) != hipSuccess) return VTB_ERR_NOMEM;
+    int rc = VTB_OK;
+    for (size_t f0 = 0; f0 < frames && rc == VTB_OK; f0 += chunk) {
+        const size_t nf = std::min(chunk, frames - f0);
+        hipLaunchKernelGGL(vtb::genk_kernel<true>, dim3(unsigned(nf)), dim3(64), ly.total, st, d_in + f0 * in_stride,
+                           in_stride, d_out + f0 * out_stride, out_stride, nf, a, ly, static_cast<uint64_t*>(ws));
+        rc = vtb::gen_status();
+    }
+    if (hipFreeAsync(ws, st) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
+    return rc;
 }
 
 }  // extern "C"
