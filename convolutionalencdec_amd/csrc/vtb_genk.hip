@@ -85,31 +85,65 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
     __syncthreads();
 
-    int cur = 0;
-    for (int t = 0; t < T; t++) {
-        const uint32_t rx = inb[t];
-        const int32_t* mc = met + cur * N;
-        int32_t* mn = met + (cur ^ 1) * N;
-        for (int r = 0; r < R; r++) {
-            const int d = r * 64 + lane;
+    if (R == 1) {
+        // N <= 64: one state per lane, metrics in a register, predecessors gathered with
+        // ds_bpermute, the lane's 2^k edge labels (time-invariant) in registers
+        const int d = lane;
+        const bool live = d < N;
+        int32_t m = live ? met[d] : 0;
+        uint32_t lab[16];
+        int srcl[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            const int src = live ? (d >> k) | (e << (kS - k)) : 0;
+            srcl[e] = src << 2;
+            lab[e] = (e < E && live) ? uint32_t(tab[(src << k) | (d & (E - 1))]) : 0u;
+        }
+        for (int t = 0; t < T; t++) {
+            const uint32_t rx = inb[t];
+            int32_t best = 0;
             int be = 0;
-            if (d < N) {
-                const int bits = d & (E - 1);
-                int32_t best = 0;
-                for (int e = 0; e < E; e++) {
-                    const int src = (d >> k) | (e << (kS - k));
-                    const int32_t pm = mc[src] + int32_t(__popc((uint32_t(tab[(src << k) | bits]) ^ rx) & nmask));
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                if (e < E) {
+                    const int32_t pm = __builtin_amdgcn_ds_bpermute(srcl[e], m) + int32_t(__popc((lab[e] ^ rx) & nmask));
                     if (e == 0 || pm < best) best = pm, be = e;  // first minimum
                 }
-                mn[d] = best;
             }
+            m = best;
             for (int j = 0; j < k; j++) {
-                const uint64_t w = __ballot((be >> j) & 1);
-                if (lane == j) dec[(size_t(t) * R + r) * k + j] = w;
+                const uint64_t w = __ballot(live && ((be >> j) & 1));
+                if (lane == j) dec[size_t(t) * k + j] = w;
             }
         }
-        cur ^= 1;
         __syncthreads();
+    } else {
+        int cur = 0;
+        for (int t = 0; t < T; t++) {
+            const uint32_t rx = inb[t];
+            const int32_t* mc = met + cur * N;
+            int32_t* mn = met + (cur ^ 1) * N;
+            for (int r = 0; r < R; r++) {
+                const int d = r * 64 + lane;
+                int be = 0;
+                if (d < N) {
+                    const int bits = d & (E - 1);
+                    int32_t best = 0;
+                    for (int e = 0; e < E; e++) {
+                        const int src = (d >> k) | (e << (kS - k));
+                        const int32_t pm = mc[src] + int32_t(__popc((uint32_t(tab[(src << k) | bits]) ^ rx) & nmask));
+                        if (e == 0 || pm < best) best = pm, be = e;  // first minimum
+                    }
+                    mn[d] = best;
+                }
+                for (int j = 0; j < k; j++) {
+                    const uint64_t w = __ballot((be >> j) & 1);
+                    if (lane == j) dec[(size_t(t) * R + r) * k + j] = w;
+                }
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
     }
 
     if (lane == 0) {  // traceback from state 0 (terminated frame)

@@ -259,6 +259,7 @@ GENK_CODES = (
     (4, 3, (0xB5D, 0x6E3, 0x9A7, 0xF19, 0x5CB)),
     (2, 5, (0x2DB, 0x1B5, 0x3A7)),
     (1, 7, (0o113, 0o171)),
+    (2, 3, (0x2B, 0x1D, 0x37)),
 )
 GENK_REF_PARAMS = {"k4_k2n3": GENK_CODES[0], "k3_k3n4": GENK_CODES[1]}
 
