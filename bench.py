@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--K", type=int, default=7, choices=(5, 7, 9))
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every CPU in this process's affinity mask)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: step i runs on stream i mod inflight (own plan and output), so one "
                          "batch's tail overlaps the next one's start")
@@ -117,7 +118,7 @@ def cpu_baseline(seconds, threads, frame_bits):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = os.cpu_count() or 1
-    threads = max(1, min(threads, avail))
+    threads = avail if threads <= 0 else max(1, min(threads, avail))
     if os.path.exists(ref):
         lib = ctypes.CDLL(ref)
         lib.ref_speed.restype = ctypes.c_double
@@ -128,12 +129,16 @@ def cpu_baseline(seconds, threads, frame_bits):
         os.dup2(2, 1)
         try:
             mbps = lib.ref_speed(seconds, threads, pkt_bytes)
-            one = lib.ref_speed(min(2.0, seconds), 1, pkt_bytes)  # also one core
+            # also one core, at the workload's frame length and at speedDecode's
+            # own 2048-bit packets (speedDecode.c:38-47)
+            one = lib.ref_speed(min(2.0, seconds), 1, pkt_bytes)
+            one_2048 = lib.ref_speed(min(2.0, seconds), 1, 256)
         finally:
             os.dup2(saved, 1)
             os.close(saved)
         return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
-                "single_core_value": round(one, 2), "cpu_model": cpu_model(),
+                "single_core_value": round(one, 2), "single_core_value_2048bit": round(one_2048, 2),
+                "cpu_model": cpu_model(), "host_cpus_available": avail,
                 "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
                           f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "
                           f"{seconds:g} s, one decoder state per thread"}
@@ -156,23 +161,37 @@ def cpu_baseline(seconds, threads, frame_bits):
                       f"{seconds:g} s on {threads} threads"}
 
 
-def load_traffic(workload_key):
-    """HBM bytes per launch measured by the rocprofv3 --pmc passes (profiles/pmc_traffic.json)."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def lib_sha16():
+    """Hash of the shipped decoder library: counter files are only valid for this binary."""
+    import hashlib
+
+    with open(os.path.join(REPO, "convolutionalencdec_amd", "lib", "libviterbi_amd.so"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def _stamped(name, workload_key):
+    """Entry `workload_key` of profiles/<name> if it was measured on this exact library
+    (tools/traffic_summary.py stamps every entry with lib_sha16), else None: counters of
+    another binary are never paired with this run's launch time."""
     try:
-        with open(path) as fh:
-            return json.load(fh).get(workload_key)
+        with open(os.path.join(REPO, "profiles", name)) as fh:
+            ent = json.load(fh).get(workload_key)
     except (OSError, ValueError):
         return None
+    if not isinstance(ent, dict) or ent.get("lib_sha16") != lib_sha16():
+        return None
+    return ent
+
+
+def load_traffic(workload_key):
+    """HBM bytes per launch measured by the rocprofv3 --pmc passes (profiles/pmc_traffic.json)."""
+    ent = _stamped("pmc_traffic.json", workload_key)
+    return None if ent is None else ent.get("bytes_per_launch")
 
 
 def load_valu(workload_key):
     """VALU wave-instructions per launch from the rocprofv3 SQ pass (profiles/pmc_valu.json)."""
-    try:
-        with open(os.path.join(REPO, "profiles", "pmc_valu.json")) as fh:
-            return json.load(fh).get(workload_key)
-    except (OSError, ValueError):
-        return None
+    return _stamped("pmc_valu.json", workload_key)
 
 
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 integer VALU instruction per 4 cycles per
@@ -313,8 +332,12 @@ def main():
     ber = float(np.unpackbits(decoded ^ unc).mean())
 
     # Average launch duration for the roofline: HIP events on the launch stream around the
-    # timed region's K back-to-back launches (what rocprofv3's per-kernel average sees).
+    # timed region's K back-to-back launches (what rocprofv3's per-kernel average sees), plus
+    # one event after every launch (per-launch min / median / max, so a slow first launch or
+    # a slow run shows in the line), and the host's issue time per launch.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    per = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if nin == 1 and not args.graph else []
+    issue = {}
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
     if args.graph and nin == 1:
         # the K steps captured as K kernel nodes of one graph (same batch, same output buffer)
@@ -327,8 +350,23 @@ def main():
         assert torch.equal(out.cpu(), torch.from_numpy(decoded))
         elapsed = timer.run(graph.replay, 1, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
     else:
-        elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+        base_step = step
+
+        def step():  # noqa: F811 -- the launch, then its end event on the launch stream
+            base_step()
+            if per:
+                per[state["i"] - 1].record(stream)
+
+        def issued():
+            issue["s"] = time.perf_counter()
+            ev1.record(stream)
+
+        state["i"] = 0
+        t_issue0 = time.perf_counter()
+        elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=issued)
+        issue["us"] = (issue["s"] - t_issue0) / args.steps * 1e6
     kern_ms = ev0.elapsed_time(ev1) / args.steps
+    launch_ms = [ev0.elapsed_time(per[0])] + [per[i - 1].elapsed_time(per[i]) for i in range(1, len(per))] if per else []
 
     def step():  # noqa: F811 -- single-stream launches (per-launch duration with --inflight > 1)
         dec.decode_device(x, out=out, stream=stream.cuda_stream)
@@ -415,6 +453,11 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 6),
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_min": round(min(launch_ms), 5) if launch_ms else None,
+            "kernel_ms_median": round(float(np.median(launch_ms)), 5) if launch_ms else None,
+            "kernel_ms_max": round(max(launch_ms), 5) if launch_ms else None,
+            "kernel_ms_first": round(launch_ms[0], 5) if launch_ms else None,
+            "host_issue_us_per_launch": round(issue["us"], 2) if "us" in issue else None,
             "algorithmic_bytes_per_launch": alg_bytes,
             # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)
             "secondary": secondary,

@@ -120,6 +120,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.frames = frames;
     a.stream = stream;
     a.cus = p->cus;
+    a.tstamp = vtb::debug_tstamp();
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
     const char* force = std::getenv("VTB_KERNEL");
     const bool any = !force || !*force;
@@ -230,6 +231,7 @@ namespace vtb {
 
 namespace {
 std::mutex g_pool_mutex;
+unsigned long long* g_tstamp = nullptr;
 hipMemPool_t g_pools[64] = {};
 }  // namespace
 
@@ -284,11 +286,18 @@ int resident_per_cu(const void* kernel, size_t lds) {
 
 hipError_t workspace_free(void* p, hipStream_t stream) { return hipFreeAsync(p, stream); }
 
+unsigned long long* debug_tstamp() { return g_tstamp; }
+void set_debug_tstamp(unsigned long long* p) { g_tstamp = p; }
+
 }  // namespace vtb
 
 extern "C" {
 
 const char* vtb_version(void) { return VTB_VERSION_STRING; }
+
+// Measurement only (not in include/viterbi_amd.h): device buffer of 8 u64 per wave that the
+// next K=7 frame launches fill with phase timestamps (tools/tstamp.py); nullptr turns it off.
+void vtb_debug_set_tstamp(unsigned long long* d_buf) { vtb::set_debug_tstamp(d_buf); }
 
 const char* vtb_strerror(int err) {
     switch (err) {

@@ -25,8 +25,17 @@ struct Launch {
     hipStream_t stream = nullptr;
     void* ws = nullptr;  // device workspace of at least *_workspace_bytes() (plan-owned)
     int cus = 256;       // compute units of the device (persistent grids)
+    // Measurement only (tools/tstamp.py, vtb_debug_set_tstamp): when set, the K=7 kernel's
+    // waves write 8 u64 per wave -- realtime (100 MHz) at entry, after the ACS, after the
+    // traceback and at exit, shader-clock at entry and exit, HW_ID and XCC_ID.  Null in
+    // production (one uniform branch per stamp).
+    unsigned long long* tstamp = nullptr;
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
+
+// The debug timestamp buffer of the next launches (nullptr: off).  Measurement only.
+unsigned long long* debug_tstamp();
+void set_debug_tstamp(unsigned long long* p);
 
 // Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
 // kernel: bit 2 skip traceback verification, bit 3 warm-up walk only, bit 4 return at entry, bit 5

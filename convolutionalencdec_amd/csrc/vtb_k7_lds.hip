@@ -86,6 +86,9 @@ constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) c
 #define VTB_EXP_TBWARM 48
 #endif
 constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
+// Share of its chunks the second-dispatched wave of a SIMD runs at priority 1 (wave balance,
+// k7_pair).  55 / 59 / 63 measured alike (31.06 / 31.1 / 31.0 us per 4,096-frame launch).
+constexpr int kPrioPct = 59;
 constexpr uint32_t kR1 = 0x10001u;
 
 // History bits per u16 half: soft input keeps 4m + h (2 history bits, the
@@ -119,6 +122,11 @@ int region0(int T) {  // multiple of 256: the traceback edits survivor-word addr
     return (r + 255) / 256 * 256;
 }
 size_t lds_bytes(int T) { return (size_t)region0(T) + 16 * (size_t)t_pad(T); }
+
+// Measurement only: phase timestamp k of this wave (Launch::tstamp, 8 u64 per wave).
+__device__ __forceinline__ void tstamp(const Launch& table, int k) {
+    if (table.tstamp && threadIdx.x == 0) table.tstamp[8 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // lane <-> location map (an involution)
 __host__ __device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ (((l >> 2) & 1u) * 3u); }
@@ -863,8 +871,26 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #undef VTB_RENORM_APPLY
 #undef VTB_RD
     };
+    // Wave balance.  The two waves of a SIMD get VALU issue by priority, then
+    // age: at equal priority the first-dispatched wave (HW_ID wave slot 0) ran its ACS 6.6 us
+    // ahead of its partner, which then ran alone at the single-wave rate (tools/tstamp.py,
+    // 4,096 frames: ACS ends at 22.0 / 28.5 us).  The second-dispatched wave takes priority 1
+    // for the first kPrioPct % of its chunks, so both finish together (ends 27.2 / 27.4 us,
+    // launch -3.5 %).  Scheduling only: decisions are unchanged.
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+#ifdef VTB_EXP_NOPRIO
+    hwid = 0;  // measurement only: age arbitration
+#endif
+    const bool second = (hwid & 1u) != 0;
+    const int hi_chunks = kPrioPct * ((tacs - tbeg) / kChunk) / 100;
+    auto prio = [&](int t0) {
+        if (second && (t0 - tbeg) / kChunk < hi_chunks) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    };
     if constexpr (SPLIT) {
         for (int t0 = 0; t0 < tacs; t0 += kChunk) {
+            prio(t0);
             acs_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
             if (t0 == kSplitWarm - kChunk) msave = M;
         }
@@ -872,15 +898,21 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         // chunks in order; only the one before the last stages padding rows
         const int tstage = tacs - 2 * kChunk;  // the chunk that stages the last one
         int t0 = tbeg;
-        for (; t0 < tstage; t0 += kChunk) acs_chunk(t0, std::false_type{});
+        for (; t0 < tstage; t0 += kChunk) {
+            prio(t0);
+            acs_chunk(t0, std::false_type{});
+        }
         if (t0 == tstage) {
+            prio(t0);
             acs_chunk(t0, std::true_type{});
             t0 += kChunk;
         }
         if (t0 < tacs) acs_chunk(t0, std::false_type{});
     }
+    __builtin_amdgcn_s_setprio(0);
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
+    tstamp(table, 1);
     if constexpr (STREAM) {
         if (!sa.last) sa.state[wp * kStreamStateWords + lane] = M;
         stream_traceback<SOFT, GS>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, uint32_t(r0));
@@ -959,6 +991,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         }
     }
     __syncthreads();
+    tstamp(table, 2);
 
     // copy the decoded bytes out (bits past L are zero: the survivor ends in state 0)
     const int nbytes = (L + 7) >> 3;
@@ -1002,6 +1035,11 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
     const size_t pairs = (frames + 1) / 2;
     uint32_t pra = 0, prb = 0;  // next pair's chunk-0 input, prefetched during the traceback (LDS variant)
     uint32_t off[6];
+    uint64_t clk0 = 0;
+    if (table.tstamp) {
+        tstamp(table, 0);
+        clk0 = __builtin_amdgcn_s_memtime();
+    }
     column_offsets(table, off);
     if constexpr (!LOOP) {
         k7_pair<SOFT, GS, STREAM, false, SPLIT>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
@@ -1012,6 +1050,19 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
                                             ws_wave, sa, wp, blockIdx.x, !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb,
                                             off);
             __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
+        }
+    }
+    if (table.tstamp) {
+        tstamp(table, 3);
+        const uint64_t clk1 = __builtin_amdgcn_s_memtime();
+        uint32_t hwid, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0) {
+            table.tstamp[8 * blockIdx.x + 4] = clk0;
+            table.tstamp[8 * blockIdx.x + 5] = clk1;
+            table.tstamp[8 * blockIdx.x + 6] = hwid;
+            table.tstamp[8 * blockIdx.x + 7] = xcc;
         }
     }
 }

@@ -7,7 +7,7 @@ build() {
   name=$1; shift
   d=convolutionalencdec_amd/lib/exp/$name; mkdir -p $d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -I$CS "$@" \
-      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_k9.hip $CS/vtb_gen.hip
+      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_k9.hip $CS/vtb_gen.hip $CS/vtb_genk.hip
 }
 for v in "$@"; do
   case $v in
@@ -24,6 +24,7 @@ for v in "$@"; do
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
     base) build base ;;
+    noprio) build noprio -DVTB_EXP_NOPRIO ;;
     tbspec) build tbspec -DVTB_EXP_TBSPEC ;;
     nonop) build nonop -DVTB_EXP_NONOP ;;
     bitop3) build bitop3 -DVTB_EXP_BITOP3 ;;

@@ -11,6 +11,7 @@ K7_soft_F4096_L1024), the same halving, so the fetch figure is doubled; WRITE_SI
 the output bytes exactly (524,288) and is used as is.
 """
 import csv
+import hashlib
 import json
 import os
 import sys
@@ -19,6 +20,10 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"  # holds pmc_fetch/, p
 rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
 key = sys.argv[3] if len(sys.argv) > 3 else "K7_soft_F4096_L1024"
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# every entry is stamped with the library it was measured on; bench.py reports null for
+# counters of any other binary
+with open(os.path.join(repo, "convolutionalencdec_amd", "lib", "libviterbi_amd.so"), "rb") as _fh:
+    LIB_SHA16 = hashlib.sha256(_fh.read()).hexdigest()[:16]
 
 
 def mean_counter(d, name):
@@ -37,14 +42,14 @@ FETCH_CORRECTION = 2.0
 total = (FETCH_CORRECTION * fetch_kib + write_kib) * 1024.0
 os.makedirs(os.path.join(repo, "profiles", rnd), exist_ok=True)
 with open(os.path.join(repo, "profiles", rnd, f"pmc_traffic_detail_{tag}.json"), "w") as fh:
-    json.dump({"workload": key, "fetch_kib_per_dispatch_raw": fetch_kib, "fetch_correction": FETCH_CORRECTION,
+    json.dump({"workload": key, "lib_sha16": LIB_SHA16, "fetch_kib_per_dispatch_raw": fetch_kib, "fetch_correction": FETCH_CORRECTION,
                "write_kib_per_dispatch": write_kib,
                "dispatches": [nf, nw], "bytes_per_launch": total}, fh, indent=1)
 path = os.path.join(repo, "profiles", "pmc_traffic.json")
 data = {}
 if os.path.exists(path):
     data = json.load(open(path))
-data[key] = round(total)
+data[key] = {"bytes_per_launch": round(total), "lib_sha16": LIB_SHA16}
 json.dump(data, open(path, "w"), indent=1, sort_keys=True)
 print(key, "fetch KiB", fetch_kib, "write KiB", write_kib, "bytes/launch", total)
 
@@ -66,6 +71,7 @@ if os.path.exists(os.path.join(root, "pmc_valu", "run_counter_collection.csv")):
     vpath = os.path.join(repo, "profiles", "pmc_valu.json")
     vd = json.load(open(vpath)) if os.path.exists(vpath) else {}
     # (effective_clock_ghz reads high on dispatches shorter than ~0.3 ms: kept in the detail file only)
-    vd[key] = {"valu_wave_insts_per_launch": round(v["SQ_INSTS_VALU"]), "waves_per_launch": round(v["SQ_WAVES"])}
+    vd[key] = {"valu_wave_insts_per_launch": round(v["SQ_INSTS_VALU"]), "waves_per_launch": round(v["SQ_WAVES"]),
+               "lib_sha16": LIB_SHA16}
     json.dump(vd, open(vpath, "w"), indent=1, sort_keys=True)
     print(key, "VALU insts/launch", v["SQ_INSTS_VALU"], "waves", v["SQ_WAVES"], "clock GHz", v["effective_clock_ghz"])
