@@ -12,7 +12,7 @@ LIB := convolutionalencdec_amd/lib
 CSRC := convolutionalencdec_amd/csrc
 
 HIP_SRCS := $(CSRC)/vtb_api.hip $(CSRC)/vtb_lds_path.hip $(CSRC)/vtb_k7_lds.hip $(CSRC)/vtb_k9.hip \
-            $(CSRC)/vtb_gen.hip $(CSRC)/vtb_genk.hip
+            $(CSRC)/vtb_gen.hip $(CSRC)/vtb_genk.hip $(CSRC)/vtb_legacy.hip
 HIP_HDRS := $(CSRC)/vtb_internal.h $(CSRC)/vtb_k7_common.h include/viterbi_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
@@ -20,7 +20,7 @@ LEGACY_SRCS := $(CSRC)/legacy/convEncode.c $(CSRC)/legacy/convHelpers.c $(CSRC)/
 LEGACY_HDRS := include/viterbiDecoder.h include/viterbiDecoderButterflyk1.h include/convEncode.h include/convHelpers.h
 LEGACY_CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wno-unused-function
 
-LEGACY_KS := 5 7 9
+LEGACY_KS := 3 5 7 9 4_k2n3 3_k3n4
 
 .PHONY: all lib legacy oracle clean
 all: lib legacy oracle

@@ -1,20 +1,25 @@
 /*
  * Legacy decoder API (include/viterbiDecoder.h, include/viterbiDecoderButterflyk1.h) on
  * top of the MI355X C ABI (include/viterbi_amd.h).  Compiled per code configuration with
- * the harness's convCodeParams.h; the trellis itself never runs here.
+ * the harness's convCodeParams.h; no trellis work runs on the host.
  *
- * VITERBI_DECODER_HARD (viterbiDecoderHardButterflyk1) contract, reference
- * src/viterbiDecoderButterflyk1.c:82-263:
+ * VITERBI_DECODER_HARD contract, reference src/viterbiDecoderButterflyk1.c:82-263 (k=1) and
+ * src/viterbiDecoder.c:52-234 (k>1):
  *   - segments of one frame may arrive over several calls with last=false; they are
  *     staged in the caller's state struct (tracebackBufs, which is large enough for
- *     MAX_PKT_LEN_SEGMENTS bytes) and `iteration` counts them;
- *   - last=true decodes the whole frame on the GPU (vtb_decode_frame_legacy), writes the
- *     information bytes, resets the state and returns the byte count.
- * Node metrics are not updated between last=false calls in this build (the GPU keeps
- * them); nodeMetricsCur holds the reset values.  Errors the reference leaves undefined
- * (more than MAX_PKT_LEN_SEGMENTS segments, a last=true frame of <= S segments) print a
- * message and return 0; a missing or failing GPU prints and exit(1)s, the reference's
- * convention for fatal configuration errors (src/viterbiDecoder.c:10-13).
+ *     MAX_PKT_LEN_SEGMENTS bytes) and `iteration` counts them.  Each such call also runs
+ *     the reference's metric update on the GPU (vtb_legacy_metrics_k1 / _genk), so
+ *     nodeMetricsCur (and, k=1, renormCounter) read exactly as in the reference between
+ *     calls (handTracedTest/handTraced.c:72-111 reads them);
+ *   - last=true decodes the whole frame on the GPU (vtb_decode_frame_legacy, k>1:
+ *     vtb_genk_decode_frame_legacy), writes the information bytes, resets the state and
+ *     returns the byte count.  For k>1 the reference would have emitted bytes during the
+ *     last=false calls through its register-exchange traceback (viterbiDecoder.c:140-190,
+ *     which drops bits for k*5K > 8); here every byte of the frame comes with last=true.
+ * Errors the reference leaves undefined (more than MAX_PKT_LEN_SEGMENTS segments, a
+ * last=true frame of <= S segments) print a message and return 0; a missing or failing GPU
+ * prints and exit(1)s, the reference's convention for fatal configuration errors
+ * (src/viterbiDecoder.c:10-13).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +28,21 @@
 #include "convEncode.h"
 #include "viterbiDecoder.h"
 #include "viterbi_amd.h"
+
+static vtb_genk_code_t legacy_genk_code(void) {
+    vtb_genk_code_t c;
+    memset(&c, 0, sizeof(c));
+    c.input_bits = k;
+    c.constraint_length = K;
+    c.coded_bits = n;
+    for (int i = 0; i < n && i < 8; i++) c.generators[i] = g[i];
+    return c;
+}
+
+static void gpu_failed(const char* what, int r) {
+    printf("viterbi: GPU %s failed: %s (%d)\n", what, vtb_strerror(r), r);
+    exit(1);
+}
 
 static vtb_code_t legacy_code(void) {
     vtb_code_t c;
@@ -127,10 +147,11 @@ void viterbiInitButterflyk1(viterbiHardState_t* state) {
 
 void resetViterbiDecoderHardButterflyk1(viterbiHardState_t* state) { reset_common(state); }
 
-/* The reference's renormalisation phase after `steps` more segments (:159-183). */
-static unsigned renorm_phase_after(unsigned counter, unsigned steps) {
-    for (unsigned i = 0; i < steps; i++) counter = counter >= 120 ? 0 : counter + 1;
-    return counter;
+METRIC_TYPE minMetricGeneric(const METRIC_TYPE (*metrics)[NUM_STATES]) {
+    METRIC_TYPE best = (*metrics)[0];
+    for (unsigned i = 1; i < NUM_STATES; i++)
+        if ((*metrics)[i] < best) best = (*metrics)[i];
+    return best;
 }
 
 static int decode_staged(viterbiHardState_t* VTB_LEGACY_RESTRICT state, const uint8_t* frame, int segments,
@@ -141,10 +162,7 @@ static int decode_staged(viterbiHardState_t* VTB_LEGACY_RESTRICT state, const ui
     }
     vtb_code_t c = legacy_code();
     int r = vtb_decode_frame_legacy(&c, frame, segments, uncoded);
-    if (r < 0) {
-        printf("viterbi: GPU decode failed: %s (%d)\n", vtb_strerror(r), r);
-        exit(1);
-    }
+    if (r < 0) gpu_failed("decode", r);
     return r;
 }
 
@@ -160,7 +178,14 @@ int viterbiDecoderHardButterflyk1(viterbiHardState_t* VTB_LEGACY_RESTRICT state,
     }
     if (!last) {
         memcpy(staged + state->iteration, codedSegments, (size_t)segmentsIn);
-        state->renormCounter = renorm_phase_after(state->renormCounter, (unsigned)segmentsIn);
+        if (segmentsIn > 0) {
+            /* the reference's uint8 metric update and renormalisation phase (:101-191) */
+            vtb_code_t c = legacy_code();
+            uint32_t counter = state->renormCounter;
+            int r = vtb_legacy_metrics_k1(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter);
+            if (r != VTB_OK) gpu_failed("metric update", r);
+            state->renormCounter = counter;
+        }
         state->iteration += (unsigned)segmentsIn;
         return 0;
     }
@@ -180,12 +205,53 @@ int viterbiDecoderHard(viterbiHardState_t* VTB_LEGACY_RESTRICT state, uint8_t* V
 #if k == 1
     return viterbiDecoderHardButterflyk1(state, codedSegments, uncoded, segmentsIn, last);
 #else
-    (void)state;
-    (void)codedSegments;
-    (void)uncoded;
-    (void)segmentsIn;
-    (void)last;
-    printf("viterbi: k=%d codes are not supported by this build\n", k);
-    exit(1);
+    /* General k (reference src/viterbiDecoder.c:52-234): frames staged as for k=1, decoded
+     * by the GPU general-k kernel with last=true. */
+    uint8_t* staged = &state->tracebackBufs[0][0];
+    const size_t capacity = sizeof(state->tracebackBufs);
+    if (segmentsIn < 0) segmentsIn = 0;
+    if ((size_t)state->iteration + (size_t)segmentsIn > (size_t)MAX_PKT_LEN_SEGMENTS ||
+        (size_t)state->iteration + (size_t)segmentsIn > capacity) {
+        printf("viterbi: frame exceeds MAX_PKT_LEN_SEGMENTS (%d); dropped\n", (int)MAX_PKT_LEN_SEGMENTS);
+        resetViterbiDecoderHard(state);
+        return 0;
+    }
+    vtb_genk_code_t c = legacy_genk_code();
+    if (!last) {
+        memcpy(staged + state->iteration, codedSegments, (size_t)segmentsIn);
+        if (segmentsIn > 0) {
+            /* the reference's metric update (:84-131): every step writes Next and swaps
+             * Cur/Next, so after segmentsIn steps Cur holds the newest metrics and Next the
+             * ones a step before */
+            uint32_t m[NUM_STATES], prev[NUM_STATES];
+            for (unsigned s = 0; s < NUM_STATES; s++) m[s] = (uint32_t)(*state->nodeMetricsCur)[s];
+            int r = vtb_legacy_metrics_genk(&c, codedSegments, segmentsIn, m, prev);
+            if (r != VTB_OK) gpu_failed("metric update", r);
+            if (segmentsIn & 1) swapViterbiArrays(state);
+            for (unsigned s = 0; s < NUM_STATES; s++) {
+                (*state->nodeMetricsCur)[s] = (METRIC_TYPE)m[s];
+                (*state->nodeMetricsNext)[s] = (METRIC_TYPE)prev[s];
+            }
+        }
+        state->iteration += (unsigned)segmentsIn;
+        return 0;
+    }
+    const uint8_t* frame = codedSegments;
+    int segments = segmentsIn;
+    if (state->iteration > 0) {
+        memcpy(staged + state->iteration, codedSegments, (size_t)segmentsIn);
+        frame = staged;
+        segments = (int)(state->iteration + (unsigned)segmentsIn);
+    }
+    int r = 0;
+    if (segments <= S || ((segments - S) * k) % 8) {
+        printf("viterbi: frame of %d segments does not hold a whole number of bytes after the %d tail segments; "
+               "nothing decoded\n", segments, S);
+    } else {
+        r = vtb_genk_decode_frame_legacy(&c, frame, segments, uncoded);
+        if (r < 0) gpu_failed("decode", r);
+    }
+    resetViterbiDecoderHard(state);
+    return r;
 #endif
 }

@@ -186,8 +186,10 @@ struct DeviceGuard {
     }
 };
 
+}  // namespace
+
 // hipGetDeviceProperties costs ~1 ms: answered once per device.
-bool device_is_gfx950(int dev) {
+bool vtb::device_is_gfx950(int dev) {
     static std::mutex mu;
     static int known[64] = {};  // 0 unknown, 1 gfx950, 2 other / failed
     if (dev < 0) return false;
@@ -203,6 +205,9 @@ bool device_is_gfx950(int dev) {
     }
     return ok;
 }
+
+namespace {
+using vtb::device_is_gfx950;
 
 // vtb_decode_host_multi's plans, one per (code, input, frame length, device), kept for the
 // process (plan creation, its allocations and the first launch's setup cost milliseconds,
@@ -658,20 +663,20 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
         vtb_plan_t* plan = nullptr;
         uint8_t* h_in = nullptr;   // pinned, T bytes
         uint8_t* h_out = nullptr;  // pinned, out_bytes(L)
-        ~Cache() {
+        void release() {
             if (h_in) (void)hipHostFree(h_in);
             if (h_out) (void)hipHostFree(h_out);
             vtb_plan_destroy(plan);
+            plan = nullptr;
+            h_in = h_out = nullptr;
         }
+        ~Cache() { release(); }
     };
     thread_local Cache cache;
     vtb_plan_t*& p = cache.plan;
-    if (!p || p->code.constraint_length != code->constraint_length || p->code.generators[0] != code->generators[0] || p->code.generators[1] != code->generators[1] || p->L != L) {
-        vtb_plan_destroy(p);
-        p = nullptr;
-        if (cache.h_in) (void)hipHostFree(cache.h_in);
-        if (cache.h_out) (void)hipHostFree(cache.h_out);
-        cache.h_in = cache.h_out = nullptr;
+    if (!p || p->code.constraint_length != code->constraint_length || p->code.generators[0] != code->generators[0] ||
+        p->code.generators[1] != code->generators[1] || p->L != L) {
+        cache.release();
         int dev = 0;
         if (const char* s = std::getenv("VTB_LEGACY_DEVICE")) dev = std::atoi(s);
         int r = vtb_plan_create(&p, code, VTB_INPUT_HARD, L, dev);
@@ -683,8 +688,10 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
         if (!g.ok || hipHostMalloc(reinterpret_cast<void**>(&cache.h_in), size_t(segments), hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void**>(&cache.h_out), out_bytes(L), hipHostMallocDefault) != hipSuccess ||
             hipMalloc(&p->d_in, size_t(segments)) != hipSuccess || hipMalloc(&p->d_out, out_bytes(L)) != hipSuccess ||
-            hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
-            return VTB_ERR_NOMEM;  // (the partial cache is released on the next call or at thread exit)
+            hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+            cache.release();  // no half-built cache survives a failure (the next call rebuilds)
+            return VTB_ERR_NOMEM;
+        }
         p->cap_frames = 1;
     }
     DeviceGuard g(p->device);

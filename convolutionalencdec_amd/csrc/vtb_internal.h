@@ -93,6 +93,9 @@ bool k9_supported(const Launch& a);
 size_t k9_workspace_bytes(const Launch& a);
 hipError_t launch_k9(const Launch& a);
 
+// True if device `dev` is a gfx950 (answered once per device: the property query costs ~1 ms).
+bool device_is_gfx950(int dev);
+
 // Stream-ordered scratch memory from a per-device pool that keeps its memory (no release
 // back to the driver between launches), so a per-launch workspace costs no hipMalloc.
 hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream);

@@ -49,6 +49,9 @@ EXPORTED_SYMBOLS = (
     "vtb_awgn_kq",
     "vtb_bsc_p32",
     "vtb_genk_decode_device",
+    "vtb_legacy_metrics_k1",
+    "vtb_legacy_metrics_genk",
+    "vtb_genk_decode_frame_legacy",
 )
 
 

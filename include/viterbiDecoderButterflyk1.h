@@ -22,6 +22,9 @@ int viterbiDecoderHardButterflyk1(viterbiHardState_t* VTB_LEGACY_RESTRICT state,
                                   uint8_t* VTB_LEGACY_RESTRICT codedSegments,
                                   uint8_t* VTB_LEGACY_RESTRICT uncoded, int segmentsIn, bool last);
 
+/* Smallest of the NUM_STATES metrics (reference :19, defined at :375-391). */
+METRIC_TYPE minMetricGeneric(const METRIC_TYPE (*metrics)[NUM_STATES]);
+
 #ifdef __cplusplus
 }
 #endif

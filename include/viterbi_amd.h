@@ -16,6 +16,10 @@
  *                            layout; soft input is the build-defined 8-bit extension)
  *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
  *                           behind include/viterbiDecoder.h (VITERBI_DECODER_HARD)
+ *   vtb_legacy_metrics_k1   the metric update of a last=false call (:101-191), so the
+ *                           legacy nodeMetricsCur reads as the reference's between calls
+ *   vtb_legacy_metrics_genk the generic decoder's metric update   src/viterbiDecoder.c:84-131
+ *   vtb_genk_decode_frame_legacy  viterbiDecoderHard, one k>1 frame  src/viterbiDecoder.c:52-234
  *   vtb_stream_*            the same function called chunk by chunk with last = false and
  *                           then last = true (:85-196 keep the state across calls), batched
  *                           over streams, with the block traceback the reference leaves TODO
@@ -230,6 +234,32 @@ typedef struct {
  * VTB_ERR_UNSUPPORTED when the trellis or the frame exceeds one CU's LDS. */
 int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const uint8_t* d_in, size_t in_stride,
                            uint8_t* d_out, size_t out_stride, size_t frames, void* stream);
+
+/* ---- Legacy per-call semantics (include/viterbiDecoder.h behind VITERBI_DECODER_HARD) ----
+ * Synchronous, host buffers, run on a per-host-thread context on device 0 (or
+ * $VTB_LEGACY_DEVICE). */
+
+/* The metric update a last=false call of the reference's k=1 decoder performs over `count`
+ * segments (viterbiDecoderHardButterflyk1, src/viterbiDecoderButterflyk1.c:101-191), so that
+ * nodeMetricsCur reads as in the reference between calls: uint8 path metrics with wrapping
+ * sums, the strict '>' select and the subtract-the-minimum renormalisation when the counter
+ * reaches 120 (:159-183).  metrics[2^(K-1)] (the reference's nodeMetricsA) and
+ * *renorm_counter are updated in place.  Like the reference, the butterfly identity is
+ * applied whatever the generators (vtb_code_check is not required). */
+int vtb_legacy_metrics_k1(const vtb_code_t* code, const uint8_t* segments, int32_t count, uint8_t* metrics,
+                          uint32_t* renorm_counter);
+
+/* The metric update of the generic decoder (viterbiDecoderHard, src/viterbiDecoder.c:84-131):
+ * destination-indexed, exact metrics, first minimum over the 2^k predecessors.  metrics[2^(k(K-1))]
+ * is updated in place; prev_metrics (optional) receives the metrics one step before the last
+ * (the reference's nodeMetricsNext after its final swap). */
+int vtb_legacy_metrics_genk(const vtb_genk_code_t* code, const uint8_t* segments, int32_t count, uint32_t* metrics,
+                            uint32_t* prev_metrics);
+
+/* One general-k hard frame of `segments` coded segments from host memory (VITERBI_DECODER_HARD
+ * for k > 1): decoded by vtb_genk_decode_device, (segments - K + 1) * k / 8 bytes written to
+ * out and returned (the reference's byte count for a whole frame), or a VTB_ERR_* code. */
+int vtb_genk_decode_frame_legacy(const vtb_genk_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out);
 
 #ifdef __cplusplus
 }

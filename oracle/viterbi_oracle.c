@@ -492,3 +492,44 @@ int oracle_genk_decode(int k, int K, int n, const uint64_t* g, const uint8_t* co
     free(dec);
     return nb;
 }
+
+/* The generic decoder's metric update over `count` segments (reference
+ * src/viterbiDecoder.c:84-131: destination-indexed, predecessors src = d/2^k + e*2^((S-1)k),
+ * path metric = source metric + Hamming distance of the edge label, first minimum), from
+ * the metrics in m[N] (updated in place); prev[N] (optional) receives the metrics one step
+ * before the last.  Exact uint32 sums: the reference's METRIC_TYPE is wide enough for
+ * MAX_PKT_LEN_SEGMENTS steps at k > 1 (viterbiDecoder.h:51-60). */
+int oracle_genk_metrics(int k, int K, int n, const uint64_t* g, const uint8_t* coded, int count, uint32_t* m,
+                        uint32_t* prev) {
+    const int S = K - 1, kS = k * S;
+    if (k < 1 || K < 2 || n < 1 || n > 8 || kS > 16 || count < 0) return -1;
+    const int N = 1 << kS, E = 1 << k;
+    uint64_t rg[8];
+    for (int i = 0; i < n; i++) rg[i] = genk_rev(g[i], k * K);
+    uint32_t* buf = malloc(sizeof(uint32_t) * 2 * (size_t)N);
+    if (!buf) return -1;
+    uint32_t *cur = buf, *nxt = buf + N;
+    memcpy(cur, m, sizeof(uint32_t) * (size_t)N);
+    memcpy(nxt, m, sizeof(uint32_t) * (size_t)N);
+    for (int t = 0; t < count; t++) {
+        const uint8_t rx = coded[t];
+        for (int d = 0; d < N; d++) {
+            const int bits = d & (E - 1);
+            uint32_t best = 0;
+            for (int e = 0; e < E; e++) {
+                const int src = (d >> k) | (e << (kS - k));
+                const uint64_t delay = ((uint64_t)src << k) | (uint64_t)bits;
+                const uint32_t pm = cur[src] + (uint32_t)__builtin_popcount((unsigned)(genk_out(n, rg, delay) ^ rx) & ((1u << n) - 1));
+                if (e == 0 || pm < best) best = pm;
+            }
+            nxt[d] = best;
+        }
+        uint32_t* x = cur;
+        cur = nxt;
+        nxt = x;
+    }
+    memcpy(m, cur, sizeof(uint32_t) * (size_t)N);
+    if (prev) memcpy(prev, nxt, sizeof(uint32_t) * (size_t)N);
+    free(buf);
+    return 0;
+}

@@ -35,6 +35,7 @@ class Oracle:
         L.oracle_encode.argtypes = [i, v, v, i, v]
         L.oracle_genk_encode.argtypes = [i, i, i, v, v, i, v]
         L.oracle_genk_decode.argtypes = [i, i, i, v, v, i, v]
+        L.oracle_genk_metrics.argtypes = [i, i, i, v, v, i, v, v]
         L.oracle_decode_hard.argtypes = [i, v, v, i, v]
         L.oracle_decode_soft.argtypes = [i, v, v, i, v]
         L.oracle_decode_batch.argtypes = [i, v, i, v, sz, i, v, sz, sz, i]
@@ -137,6 +138,15 @@ class Oracle:
             assert self.L.oracle_genk_decode(k, K, len(g), G, vp(row), info_bits, vp(o)) == info_bits // 8
             out[f] = o
         return out
+
+    def genk_metrics(self, k, K, g, coded, metrics):
+        """The generic decoder's metric update (oracle_genk_metrics): (metrics, prev)."""
+        m = np.ascontiguousarray(metrics, np.uint32).copy()
+        prev = np.zeros_like(m)
+        G = (ctypes.c_uint64 * 8)(*[int(v) for v in g])
+        row = np.ascontiguousarray(coded, np.uint8)
+        assert self.L.oracle_genk_metrics(k, K, len(g), G, vp(row), len(row), vp(m), vp(prev)) == 0
+        return m, prev
 
     def decode(self, K, g, frames, L, soft=False, threads=8):
         x = np.ascontiguousarray(frames, np.uint8)
@@ -262,6 +272,36 @@ GENK_CODES = (
     (2, 3, (0x2B, 0x1D, 0x37)),
 )
 GENK_REF_PARAMS = {"k4_k2n3": GENK_CODES[0], "k3_k3n4": GENK_CODES[1]}
+
+
+def legacy_layout(k, K, n):
+    """Byte offsets of viterbiHardState_t (include/viterbiDecoder.h, the reference's
+    src/viterbiDecoder.h:103-146 layout) for a code configuration, as the C compiler lays
+    it out (tests/test_legacy_abi.py checks this against a compiled probe)."""
+    N, E = 1 << (k * (K - 1)), 1 << k
+    if k == 1:
+        mb = 1
+    else:
+        span = n * (16 * 1024 + K - 1)
+        mb = 1 if span <= 1 << 8 else 2 if span <= 1 << 16 else 4
+
+    def align(x, a):
+        return (x + a - 1) // a * a
+
+    off = N // 2 + E * N  # edgeCodedBitsSymm, edgeCodedBits (uint8)
+    lay = {"N": N, "metric_bytes": mb}
+    lay["nodeMetricsA"] = off = align(off, 64)
+    lay["traceBackA"] = off = align(off + N * mb, 64)
+    lay["nodeMetricsB"] = off = align(off + N, mb)
+    lay["traceBackB"] = off = off + N * mb
+    lay["nodeMetricsCur"] = off = align(off + N, 8)
+    lay["traceBackCur"], lay["nodeMetricsNext"], lay["traceBackNext"] = off + 8, off + 16, off + 24
+    lay["iteration"] = off + 32
+    lay["renormCounter"] = off + 36
+    lay["decodeCarryOverCount"] = off + 41
+    lay["tracebackBufs"] = off = align(off + 42, 64)
+    lay["sizeof"] = align(off + (16 * 1024 + (K - 1) * k) * N, 64)
+    return lay
 
 
 def genk_frames(orc, k, K, g, info_bits, F, p, seed):

@@ -103,3 +103,35 @@ def test_genk_abi_argument_checks():
     assert call(native.VtbGenKCode.make(2, 4, (0x1B5, 1, 1)), 1024) == native.VTB_ERR_INVALID  # generator > 2^(kK)
     assert call(native.VtbGenKCode.make(3, 4, (0x1B5, 1, 1)), 1032) == native.VTB_ERR_UNSUPPORTED  # 512 states
     assert lib.vtb_genk_decode_device(ctypes.byref(c), 1024, buf, 600, buf, 128, 0, None) == native.VTB_OK
+
+
+@pytest.mark.parametrize("name", sorted(GENK_REF_PARAMS))
+def test_genk_metrics_match_reference_generic_decoder(orc, name):
+    """oracle_genk_metrics against the reference's own viterbiDecoderHard metric update
+    (tests/golden/genk_metrics.npz: nodeMetricsCur after every 7-segment last=false chunk)."""
+    from helpers import load_golden
+
+    z = load_golden("genk_metrics.npz")
+    k, K, g = GENK_REF_PARAMS[name]
+    N = 1 << (k * (K - 1))
+    for f in range(4):
+        rx, met = z[f"{name}_f{f}_rx"], z[f"{name}_f{f}_metrics"]
+        m = np.array([0] + [(N + 1) & 255] * (N - 1), np.uint32)
+        for c in range(met.shape[0]):
+            m, _ = orc.genk_metrics(k, K, g, rx[7 * c:7 * (c + 1)], m)
+            assert (m == met[c]).all(), (name, f, c)
+
+
+def test_genk_metrics_end_on_the_ml_path_metric(orc):
+    """Size-independent property: after a whole terminated frame, state 0's metric is the
+    Hamming distance between the received segments and the re-encoded ML decode."""
+    k, K, g = GENK_CODES[0]
+    L = 1024
+    unc, rx = genk_frames(orc, k, K, g, L, 3, 0.05, 21)
+    N = 1 << (k * (K - 1))
+    dec = orc.genk_decode(k, K, g, rx, L)
+    re = orc.genk_encode(k, K, g, dec)
+    for f in range(3):
+        m, _ = orc.genk_metrics(k, K, g, rx[f], np.array([0] + [(N + 1) & 255] * (N - 1), np.uint32))
+        dist = sum(int(bin(int(a) ^ int(b)).count("1")) for a, b in zip(rx[f], re[f]))
+        assert m[0] == dist

@@ -125,3 +125,39 @@ def test_calc_hamming_dist():
     assert lib.calcHammingDist(0b11, 0b00, 2) == 2
     assert lib.calcHammingDist(0xFF, 0x00, 2) == 2  # only the low `bits` bits count
     assert lib.calcHammingDist(0xF0, 0x0F, 8) == 8
+
+
+LEGACY_CONFIGS = {"k3": (1, 3, 2), "k5": (1, 5, 2), "k7": (1, 7, 2), "k9": (1, 9, 2), "k4_k2n3": (2, 4, 3),
+                  "k3_k3n4": (3, 3, 4)}
+
+
+@pytest.mark.parametrize("name", sorted(LEGACY_CONFIGS))
+def test_layout_helper_matches_compiled_struct(tmp_path, name):
+    """tests/helpers.legacy_layout (used by the GPU legacy tests to read nodeMetricsCur and
+    renormCounter out of the caller's state struct) against the compiler's layout."""
+    from helpers import legacy_layout
+
+    got = list(map(int, _probe(tmp_path, os.path.join(REPO, "include"), os.path.join(REPO, "params", name))))
+    lay = legacy_layout(*LEGACY_CONFIGS[name])
+    assert got[:9] == [lay[f] for f in ("sizeof", "nodeMetricsA", "traceBackA", "nodeMetricsB", "nodeMetricsCur",
+                                        "iteration", "renormCounter", "decodeCarryOverCount", "tracebackBufs")]
+    assert got[-1] == lay["N"]
+
+
+def _defined(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[2] for ln in out.splitlines() if len(ln.split()) == 3 and ln.split()[1] == "T"}
+
+
+@pytest.mark.parametrize("ref,ours", [("libref_k7.so", "k7"), ("libref_k9.so", "k9"),
+                                      ("librefgenk_k4_k2n3.so", "k4_k2n3")])
+def test_drop_in_exports_every_reference_symbol(ref, ours):
+    """Every function the reference library defines (src/*.c compiled by oracle/Makefile,
+    minus the test shim's own ref*_ entry points) is exported by the drop-in."""
+    path = os.path.join(REPO, "oracle", "_ref", ref)
+    if not os.path.exists(path):
+        pytest.skip("reference build not present (oracle/Makefile ref)")
+    want = {s for s in _defined(path) if not s.startswith(("ref_", "refgenk_", "refenc_"))}
+    assert "minMetricGeneric" in want and "viterbiDecoderHard" in want
+    missing = want - _defined(os.path.join(LIB_DIR, f"libviterbi_legacy_{ours}.so"))
+    assert not missing, sorted(missing)
