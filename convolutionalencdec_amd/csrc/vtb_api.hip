@@ -427,6 +427,13 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
         if (hipMalloc(&plan->d_out, frames * ob) != hipSuccess) return VTB_ERR_NOMEM;
         plan->cap_frames = frames;
     }
+    // After the first asynchronous operation every error exit drains both streams first:
+    // queued copies still read h_in / write h_out, which the caller may free on error.
+    auto fail = [&](int e) {
+        if (plan->copy_stream) (void)hipStreamSynchronize(plan->copy_stream);
+        (void)hipStreamSynchronize(plan->stream);
+        return e;
+    };
     // Large batches in chunks: the H2D copy of chunk i + 1 (copy stream) overlaps the decode of
     // chunk i (plan stream); every output copy follows its chunk's decode.  Small batches (one
     // launch round) in one piece.
@@ -434,11 +441,11 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
     const size_t nch = frames <= 2 * kChunkFrames ? 1 : (frames + kChunkFrames - 1) / kChunkFrames;
     if (nch == 1) {
         if (hipMemcpyAsync(plan->d_in, h_in, frames * ib, hipMemcpyHostToDevice, plan->stream) != hipSuccess)
-            return VTB_ERR_DEVICE;
+            return fail(VTB_ERR_DEVICE);
         int e = launch(plan, plan->d_in, ib, plan->d_out, ob, frames, plan->stream);
-        if (e != VTB_OK) return e;
+        if (e != VTB_OK) return fail(e);
         if (hipMemcpyAsync(h_out, plan->d_out, frames * ob, hipMemcpyDeviceToHost, plan->stream) != hipSuccess)
-            return VTB_ERR_DEVICE;
+            return fail(VTB_ERR_DEVICE);
         return hipStreamSynchronize(plan->stream) == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
     }
     if (!plan->copy_stream && hipStreamCreateWithFlags(&plan->copy_stream, hipStreamNonBlocking) != hipSuccess)
@@ -455,21 +462,21 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
                 hipSuccess ||
             hipEventRecord(copied, plan->copy_stream) != hipSuccess ||
             hipStreamWaitEvent(plan->stream, copied, 0) != hipSuccess)
-            return VTB_ERR_DEVICE;
+            return fail(VTB_ERR_DEVICE);
         int e = launch(plan, plan->d_in + lo * ib, ib, plan->d_out + lo * ob, ob, n, plan->stream);
-        if (e != VTB_OK) return e;
-        if (hipEventRecord(decoded, plan->stream) != hipSuccess) return VTB_ERR_DEVICE;
+        if (e != VTB_OK) return fail(e);
+        if (hipEventRecord(decoded, plan->stream) != hipSuccess) return fail(VTB_ERR_DEVICE);
     }
     for (size_t i = 0; i < nch; i++) {
         const size_t lo = i * kChunkFrames, n = frames - lo < kChunkFrames ? frames - lo : kChunkFrames;
         if (hipStreamWaitEvent(plan->copy_stream, plan->events[2 * i + 1], 0) != hipSuccess ||
             hipMemcpyAsync(h_out + lo * ob, plan->d_out + lo * ob, n * ob, hipMemcpyDeviceToHost,
                            plan->copy_stream) != hipSuccess)
-            return VTB_ERR_DEVICE;
+            return fail(VTB_ERR_DEVICE);
     }
-    return hipStreamSynchronize(plan->copy_stream) == hipSuccess && hipStreamSynchronize(plan->stream) == hipSuccess
-               ? VTB_OK
-               : VTB_ERR_DEVICE;
+    const bool ok_copy = hipStreamSynchronize(plan->copy_stream) == hipSuccess;
+    const bool ok_dec = hipStreamSynchronize(plan->stream) == hipSuccess;
+    return ok_copy && ok_dec ? VTB_OK : VTB_ERR_DEVICE;
 }
 
 int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,

@@ -206,8 +206,9 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     // workspace from the stream's pool, up to 1 GiB per launch (frames in launches of that)
     const size_t per = std::max<size_t>(1, (size_t(1) << 30) / dec_bytes);
     const size_t chunk = std::min(frames, per);
+    // (the per-device pool that keeps its memory between launches, vtb_api.hip workspace_alloc)
     void* ws = nullptr;
-    if (hipMallocAsync(&ws, chunk * dec_bytes, st) != hipSuccess) return VTB_ERR_NOMEM;
+    if (vtb::workspace_alloc(&ws, chunk * dec_bytes, st) != hipSuccess) return VTB_ERR_NOMEM;
     int rc = VTB_OK;
     for (size_t f0 = 0; f0 < frames && rc == VTB_OK; f0 += chunk) {
         const size_t nf = std::min(chunk, frames - f0);
@@ -215,7 +216,7 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
                            in_stride, d_out + f0 * out_stride, out_stride, nf, a, ly, static_cast<uint64_t*>(ws));
         rc = vtb::gen_status();
     }
-    if (hipFreeAsync(ws, st) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
+    if (vtb::workspace_free(ws, st) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
     return rc;
 }
 

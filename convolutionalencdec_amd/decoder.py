@@ -94,12 +94,18 @@ class ViterbiDecoder:
 
         if frames.dtype != torch.uint8 or not frames.is_cuda:
             raise TypeError("decode_device expects a torch.uint8 tensor on a ROCm device")
+        if frames.device.index != self.device:
+            raise ValueError(f"frames are on {frames.device}, the plan on cuda:{self.device}")
         x = frames.reshape(frames.shape[0], -1)
         if x.shape[1] != self.in_bytes or x.stride(1) != 1:
             raise ValueError(f"expected rows of {self.in_bytes} contiguous bytes, got {tuple(x.shape)}")
         F = x.shape[0]
         if out is None:
             out = torch.empty((F, self.out_bytes), dtype=torch.uint8, device=frames.device)
+        elif (out.dtype != torch.uint8 or out.device != frames.device or out.dim() != 2 or out.shape[0] < F
+              or out.shape[1] < self.out_bytes or out.stride(1) != 1):
+            raise ValueError(f"out must be a uint8 [>= {F}, >= {self.out_bytes}] tensor with contiguous rows on "
+                             f"{frames.device}")
         if stream is None:
             stream = torch.cuda.current_stream(frames.device).cuda_stream
         native.check(
@@ -241,6 +247,10 @@ class GenKDecoder:
         F = x.shape[0]
         if out is None:
             out = torch.empty((F, self.out_bytes), dtype=torch.uint8, device=frames.device)
+        elif (out.dtype != torch.uint8 or out.device != frames.device or out.dim() != 2 or out.shape[0] < F
+              or out.shape[1] < self.out_bytes or out.stride(1) != 1):
+            raise ValueError(f"out must be a uint8 [>= {F}, >= {self.out_bytes}] tensor with contiguous rows on "
+                             f"{frames.device}")
         if stream is None:
             stream = torch.cuda.current_stream(frames.device).cuda_stream
         with torch.cuda.device(frames.device):

@@ -24,9 +24,10 @@ def payload(frames, frame_bits, seed, device=0, stream=None):
 
     nb = (int(frame_bits) + 7) // 8
     out = torch.empty((int(frames), nb), dtype=torch.uint8, device=f"cuda:{device}")
-    native.check(native.lib().vtb_payload_device(int(seed), int(frame_bits), ctypes.c_void_p(out.data_ptr()), nb,
-                                                 int(frames), ctypes.c_void_p(_stream(out, stream))),
-                 "vtb_payload_device")
+    with torch.cuda.device(out.device):  # the kernels run on the current HIP device
+        native.check(native.lib().vtb_payload_device(int(seed), int(frame_bits), ctypes.c_void_p(out.data_ptr()), nb,
+                                                     int(frames), ctypes.c_void_p(_stream(out, stream))),
+                     "vtb_payload_device")
     return out
 
 
@@ -40,10 +41,13 @@ def encode(code, frame_bits, unc, stream=None):
     T = int(frame_bits) + code.S
     out = torch.empty((unc.shape[0], T), dtype=torch.uint8, device=unc.device)
     c = code._c()
-    native.check(native.lib().vtb_encode_device(ctypes.byref(c), int(frame_bits), ctypes.c_void_p(unc.data_ptr()),
-                                                unc.stride(0), ctypes.c_void_p(out.data_ptr()), T, unc.shape[0],
-                                                ctypes.c_void_p(_stream(unc, stream))),
-                 "vtb_encode_device")
+    if unc.stride(1) != 1:
+        unc = unc.contiguous()
+    with torch.cuda.device(unc.device):
+        native.check(native.lib().vtb_encode_device(ctypes.byref(c), int(frame_bits), ctypes.c_void_p(unc.data_ptr()),
+                                                    unc.stride(0), ctypes.c_void_p(out.data_ptr()), T, unc.shape[0],
+                                                    ctypes.c_void_p(_stream(unc, stream))),
+                     "vtb_encode_device")
     return out
 
 
@@ -53,12 +57,15 @@ def channel(coded, soft, param, seed, stream=None):
     import torch
 
     F, T = coded.shape
+    if coded.stride(1) != 1:
+        coded = coded.contiguous()
     out = torch.empty((F, T, 2) if soft else (F, T), dtype=torch.uint8, device=coded.device)
-    native.check(native.lib().vtb_channel_device(native.VTB_INPUT_SOFT8 if soft else native.VTB_INPUT_HARD,
-                                                 float(param), int(seed), ctypes.c_void_p(coded.data_ptr()),
-                                                 coded.stride(0), T, ctypes.c_void_p(out.data_ptr()),
-                                                 out.stride(0), F, ctypes.c_void_p(_stream(coded, stream))),
-                 "vtb_channel_device")
+    with torch.cuda.device(coded.device):
+        native.check(native.lib().vtb_channel_device(native.VTB_INPUT_SOFT8 if soft else native.VTB_INPUT_HARD,
+                                                     float(param), int(seed), ctypes.c_void_p(coded.data_ptr()),
+                                                     coded.stride(0), T, ctypes.c_void_p(out.data_ptr()),
+                                                     out.stride(0), F, ctypes.c_void_p(_stream(coded, stream))),
+                     "vtb_channel_device")
     return out
 
 
