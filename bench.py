@@ -316,12 +316,15 @@ def main():
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nin - 1)]
     dec, out = decs[0], outs[0]
+    # one bound launcher per batch in flight: the C ABI call with its arguments validated once
+    # (ViterbiDecoder.bind), so a step costs the host only the launch itself
+    launchers = [decs[i].bind(x, outs[i], streams[i].cuda_stream) for i in range(nin)]
     state = {"i": 0}
 
     def step():
         i = state["i"] % nin
         state["i"] += 1
-        decs[i].decode_device(x, out=outs[i], stream=streams[i].cuda_stream)
+        launchers[i]()
 
     for _ in range(args.warmup):
         step()
@@ -332,11 +335,10 @@ def main():
     ber = float(np.unpackbits(decoded ^ unc).mean())
 
     # Average launch duration for the roofline: HIP events on the launch stream around the
-    # timed region's K back-to-back launches (what rocprofv3's per-kernel average sees), plus
-    # one event after every launch (per-launch min / median / max, so a slow first launch or
-    # a slow run shows in the line), and the host's issue time per launch.
+    # timed region's K back-to-back launches (nothing else is enqueued between them: an event
+    # after every launch opens a ~3-6 us gap before the next kernel), and the
+    # host's issue time per launch.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    per = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if nin == 1 and not args.graph else []
     issue = {}
     timer = Timer(world, lambda: torch.cuda.synchronize(dev), barrier, allreduce_max)
     if args.graph and nin == 1:
@@ -350,13 +352,6 @@ def main():
         assert torch.equal(out.cpu(), torch.from_numpy(decoded))
         elapsed = timer.run(graph.replay, 1, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
     else:
-        base_step = step
-
-        def step():  # noqa: F811 -- the launch, then its end event on the launch stream
-            base_step()
-            if per:
-                per[state["i"] - 1].record(stream)
-
         def issued():
             issue["s"] = time.perf_counter()
             ev1.record(stream)
@@ -366,19 +361,27 @@ def main():
         elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=issued)
         issue["us"] = (issue["s"] - t_issue0) / args.steps * 1e6
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    launch_ms = [ev0.elapsed_time(per[0])] + [per[i - 1].elapsed_time(per[i]) for i in range(1, len(per))] if per else []
 
-    def step():  # noqa: F811 -- single-stream launches (per-launch duration with --inflight > 1)
-        dec.decode_device(x, out=out, stream=stream.cuda_stream)
-
+    one = launchers[0]
     if nin > 1:
         # the timed region interleaves streams: time K launches on one stream instead
         ev0.record(stream)
         for _ in range(args.steps):
-            step()
+            one()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         kern_ms = ev0.elapsed_time(ev1) / args.steps
+
+    # Per-launch spread, measured after the timed region (untimed): the same K launches with an
+    # event after each.  Those events add a gap before every next launch, so this pass reads
+    # slightly slower per launch than kernel_ms; it shows whether single launches are slow.
+    per = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    per[0].record(stream)
+    for i in range(args.steps):
+        one()
+        per[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    launch_ms = [per[i].elapsed_time(per[i + 1]) for i in range(args.steps)]
 
     # PCIe-inclusive rate: the same batch from pageable host memory through
     # vtb_decode_host (H2D copy, decode, D2H copy, synchronise); reported beside, never `value`.
@@ -453,10 +456,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 6),
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 5),
-            "kernel_ms_min": round(min(launch_ms), 5) if launch_ms else None,
-            "kernel_ms_median": round(float(np.median(launch_ms)), 5) if launch_ms else None,
-            "kernel_ms_max": round(max(launch_ms), 5) if launch_ms else None,
-            "kernel_ms_first": round(launch_ms[0], 5) if launch_ms else None,
+            "per_launch_pass_ms": {"min": round(min(launch_ms), 5), "median": round(float(np.median(launch_ms)), 5),
+                                   "max": round(max(launch_ms), 5), "first": round(launch_ms[0], 5),
+                                   "note": "untimed pass after the timed region, an event after every launch"},
             "host_issue_us_per_launch": round(issue["us"], 2) if "us" in issue else None,
             "algorithmic_bytes_per_launch": alg_bytes,
             # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)

@@ -177,8 +177,14 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
 struct DeviceGuard {
     int prev = -1;
     bool ok = false;
+    // Switches only when the calling thread is on another device (per-launch host cost).
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev == dev) {
+            prev = -1;
+            ok = true;
+            return;
+        }
         ok = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {

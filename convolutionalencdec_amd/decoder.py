@@ -114,6 +114,28 @@ class ViterbiDecoder:
             "vtb_decode_device")
         return out
 
+    def bind(self, frames, out, stream=None):
+        """Validate (frames, out, stream) once and return a zero-argument callable that
+        launches the decode of `frames` into `out` (vtb_decode_device) with no per-call
+        Python checks: the repeated-batch launch of a serving loop or a bench.  The caller
+        keeps both tensors alive and unchanged in shape while the callable is used."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        self.decode_device(frames, out=out, stream=stream)  # validates, and warms the plan
+        x = frames.reshape(frames.shape[0], -1)
+        fn = native.lib().vtb_decode_device
+        args = (self._plan, ctypes.c_void_p(x.data_ptr()), x.stride(0), ctypes.c_void_p(out.data_ptr()),
+                out.stride(0), x.shape[0], ctypes.c_void_p(stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc < 0:
+                raise native.VtbError(rc, "vtb_decode_device")
+
+        return launch
+
     # -- host path ---------------------------------------------------------------------
     def decode_host(self, frames):
         x = np.ascontiguousarray(frames, dtype=np.uint8).reshape(-1, self.in_bytes)
