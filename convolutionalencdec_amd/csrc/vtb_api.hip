@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -39,6 +41,13 @@ struct vtb_plan {
     void* ws = nullptr;
     size_t ws_bytes = 0;
     int cus = 256;  // compute units of the device (kernel choice)
+    // synchronous single-frame path (vtb_decode_frame_sync): coherent host-mapped buffers the
+    // kernel reads and writes directly, and its completion word
+    uint8_t* lat_in = nullptr;
+    uint8_t* lat_out = nullptr;
+    uint32_t* lat_done = nullptr;
+    int seg_waves = 0;  // SEG kernel waves (0: not usable for this plan)
+    int seg_warm = 0;
 };
 
 // Streaming decoder (include/viterbi_amd.h "Streaming decode"): all streams advance in
@@ -106,6 +115,9 @@ bool env_flag_is(const char* name, const char* value) {
 
 // Which kernel family a plan uses (see below).  VTB_KERNEL=k7|gws|k9|lds forces one (testing
 // and A/B measurement); a forced kernel that does not support the shape is an error.
+// (VTB_KERNEL=seg leaves the choice here free and only forbids nothing: the single-frame
+// path's SEG kernel is chosen in vtb_decode_frame_sync, and any other forced family turns it
+// off there.)
 int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
            size_t frames, hipStream_t stream) {
     vtb::Launch a;
@@ -123,7 +135,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.tstamp = vtb::debug_tstamp();
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
     const char* force = std::getenv("VTB_KERNEL");
-    const bool any = !force || !*force;
+    const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");  // (seg: vtb_decode_frame_sync)
     const bool want_k7 = any || env_flag_is("VTB_KERNEL", "k7");
     const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
     const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
@@ -310,6 +322,13 @@ const char* vtb_version(void) { return VTB_VERSION_STRING; }
 // next K=7 frame launches fill with phase timestamps (tools/tstamp.py); nullptr turns it off.
 void vtb_debug_set_tstamp(unsigned long long* d_buf) { vtb::set_debug_tstamp(d_buf); }
 
+// Testing only (not in include/viterbi_amd.h): how vtb_decode_frame_sync calls ended, SEG
+// kernel decoded / SEG not converged (re-decoded) / no SEG kernel for the plan.
+static std::atomic<unsigned long long> g_seg_stats[3];
+void vtb_debug_seg_stats(unsigned long long* out3) {
+    for (int i = 0; i < 3; i++) out3[i] = g_seg_stats[i].load();
+}
+
 const char* vtb_strerror(int err) {
     switch (err) {
         case VTB_OK: return "ok";
@@ -392,6 +411,12 @@ void vtb_plan_destroy(vtb_plan_t* plan) {
     DeviceGuard g(plan->device);
     if (plan->d_in) (void)hipFree(plan->d_in);
     if (plan->d_out) (void)hipFree(plan->d_out);
+    if (plan->lat_in || plan->lat_out || plan->lat_done) {
+        if (plan->stream) (void)hipStreamSynchronize(plan->stream);
+        if (plan->lat_in) (void)hipHostFree(plan->lat_in);
+        if (plan->lat_out) (void)hipHostFree(plan->lat_out);
+        if (plan->lat_done) (void)hipHostFree(plan->lat_done);
+    }
     if (plan->ws) {
         (void)hipDeviceSynchronize();  // launches on any stream may still use it
         (void)vtb::workspace_free(plan->ws, nullptr);
@@ -662,34 +687,118 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
     return VTB_OK;
 }
 
+int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out) {
+    if (!plan || !h_in || !h_out) return VTB_ERR_INVALID;
+    DeviceGuard g(plan->device);
+    if (!g.ok) return VTB_ERR_DEVICE;
+    const size_t ib = in_bytes(&plan->code, plan->input, plan->L), ob = out_bytes(plan->L);
+    if (!plan->stream && hipStreamCreateWithFlags(&plan->stream, hipStreamNonBlocking) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    if (!plan->lat_in) {
+        // coherent (fine-grained) host memory: the kernel's reads see this call's bytes and its
+        // writes reach the host without a cache flush; input padded to the kernel's 16-byte loads
+        const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+        if (hipHostMalloc(reinterpret_cast<void**>(&plan->lat_in), (ib + 32) / 16 * 16, fl) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&plan->lat_out), ob + 16, fl) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&plan->lat_done), 64, fl) != hipSuccess) {
+            if (plan->lat_in) (void)hipHostFree(plan->lat_in);
+            if (plan->lat_out) (void)hipHostFree(plan->lat_out);
+            if (plan->lat_done) (void)hipHostFree(plan->lat_done);
+            plan->lat_in = plan->lat_out = nullptr;
+            plan->lat_done = nullptr;
+            return VTB_ERR_NOMEM;
+        }
+        std::memset(plan->lat_in, 0, (ib + 32) / 16 * 16);
+        // SEG kernel geometry, read once per plan ($VTB_SEG_WAVES / $VTB_SEG_WARM: measurement)
+        int waves = 4, warm = vtb::kSegWarm;
+        if (const char* v = std::getenv("VTB_SEG_WAVES")) waves = std::atoi(v);
+        if (const char* v = std::getenv("VTB_SEG_WARM")) warm = std::atoi(v);
+        vtb::Launch a;
+        a.S = plan->code.constraint_length - 1;
+        a.soft = plan->input == VTB_INPUT_SOFT8;
+        a.T = plan->T;
+        a.L = plan->L;
+        const char* force = std::getenv("VTB_KERNEL");
+        const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");
+        plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
+        plan->seg_warm = warm;
+    }
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    uint32_t* d_done = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_in), plan->lat_in, 0) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out), plan->lat_out, 0) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_done), plan->lat_done, 0) != hipSuccess)
+        return VTB_ERR_DEVICE;
+    std::memcpy(plan->lat_in, h_in, ib);
+    volatile uint32_t* done = plan->lat_done;
+    uint32_t status = 0;
+    if (plan->seg_waves > 0) {
+        *done = 0;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        vtb::Launch a;
+        a.S = plan->code.constraint_length - 1;
+        a.soft = plan->input == VTB_INPUT_SOFT8;
+        a.T = plan->T;
+        a.L = plan->L;
+        a.in = d_in;
+        a.in_stride = ib;
+        a.out = d_out;
+        a.out_stride = ob;
+        a.frames = 1;
+        a.stream = plan->stream;
+        a.cus = plan->cus;
+        std::memcpy(a.symm, plan->symm, sizeof(a.symm));
+        if (vtb::launch_k7_seg(a, plan->seg_waves, plan->seg_warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+        // wait on the completion word (the kernel's last write); a call that takes longer than
+        // ~2 ms (first launch: code-object load) synchronises the stream instead
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0; (status = *done) == 0; spin++) {
+            if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                if (hipStreamSynchronize(plan->stream) != hipSuccess) return VTB_ERR_DEVICE;
+                status = *done;
+                if (status == 0) return VTB_ERR_DEVICE;  // finished without reporting
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    g_seg_stats[status == 1 ? 0 : status == 2 ? 1 : 2]++;
+    if (status != 1) {
+        // not converged (status 2) or no SEG kernel for this plan: the frame kernel, input from
+        // the same host-mapped buffer through one copy, output written straight to host memory
+        if (!plan->d_in && hipMalloc(&plan->d_in, ib) != hipSuccess) return VTB_ERR_NOMEM;
+        if (plan->cap_frames < 1) plan->cap_frames = 1;
+        if (hipMemcpyAsync(plan->d_in, plan->lat_in, ib, hipMemcpyHostToDevice, plan->stream) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        int r = launch(plan, plan->d_in, ib, d_out, ob, 1, plan->stream);
+        if (r != VTB_OK) {
+            (void)hipStreamSynchronize(plan->stream);
+            return r;
+        }
+        if (hipStreamSynchronize(plan->stream) != hipSuccess) return VTB_ERR_DEVICE;
+    }
+    std::memcpy(h_out, plan->lat_out, ob);
+    return VTB_OK;
+}
+
 int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out) {
     if (!code || !coded || !out) return VTB_ERR_INVALID;
     int e = check_code(code);
     if (e != VTB_OK) return e;
     const int32_t L = segments - (code->constraint_length - 1);
     if (L < 1) return VTB_ERR_INVALID;
-    // One cached plan per host thread (the reference API is reentrant per state struct), with
-    // pinned staging for the frame: the copies are DMA transfers queued behind each other on
-    // the plan's stream with the decode, and one synchronisation ends the call (a synchronous
-    // single-frame call is latency-bound: pageable copies cost ~2x the round trip).
+    // One cached plan per host thread (the reference API is reentrant per state struct); the
+    // frame goes through the plan's synchronous single-frame path.
     struct Cache {
         vtb_plan_t* plan = nullptr;
-        uint8_t* h_in = nullptr;   // pinned, T bytes
-        uint8_t* h_out = nullptr;  // pinned, out_bytes(L)
-        void release() {
-            if (h_in) (void)hipHostFree(h_in);
-            if (h_out) (void)hipHostFree(h_out);
-            vtb_plan_destroy(plan);
-            plan = nullptr;
-            h_in = h_out = nullptr;
-        }
-        ~Cache() { release(); }
+        ~Cache() { vtb_plan_destroy(plan); }
     };
     thread_local Cache cache;
     vtb_plan_t*& p = cache.plan;
     if (!p || p->code.constraint_length != code->constraint_length || p->code.generators[0] != code->generators[0] ||
         p->code.generators[1] != code->generators[1] || p->L != L) {
-        cache.release();
+        vtb_plan_destroy(p);
+        p = nullptr;
         int dev = 0;
         if (const char* s = std::getenv("VTB_LEGACY_DEVICE")) dev = std::atoi(s);
         int r = vtb_plan_create(&p, code, VTB_INPUT_HARD, L, dev);
@@ -697,30 +806,14 @@ int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_
             p = nullptr;
             return r;
         }
-        DeviceGuard g(p->device);
-        if (!g.ok || hipHostMalloc(reinterpret_cast<void**>(&cache.h_in), size_t(segments), hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&cache.h_out), out_bytes(L), hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(&p->d_in, size_t(segments)) != hipSuccess || hipMalloc(&p->d_out, out_bytes(L)) != hipSuccess ||
-            hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
-            cache.release();  // no half-built cache survives a failure (the next call rebuilds)
-            return VTB_ERR_NOMEM;
-        }
-        p->cap_frames = 1;
     }
-    DeviceGuard g(p->device);
-    if (!g.ok) return VTB_ERR_DEVICE;
-    const size_t ob = out_bytes(L);
-    std::memcpy(cache.h_in, coded, size_t(segments));
-    if (hipMemcpyAsync(p->d_in, cache.h_in, size_t(segments), hipMemcpyHostToDevice, p->stream) != hipSuccess)
-        return VTB_ERR_DEVICE;
-    // the kernel writes the decoded bytes straight into the pinned host buffer (no D2H copy;
-    // visible to the host once the stream has synchronised)
-    uint8_t* d_out = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out), cache.h_out, 0) != hipSuccess) return VTB_ERR_DEVICE;
-    int r = launch(p, p->d_in, size_t(segments), d_out, ob, 1, p->stream);
-    if (r != VTB_OK) return r;
-    if (hipStreamSynchronize(p->stream) != hipSuccess) return VTB_ERR_DEVICE;
-    std::memcpy(out, cache.h_out, ob);
+    int r = vtb_decode_frame_sync(p, coded, out);
+    if (r != VTB_OK) {
+        // no half-built state survives a failure (the next call rebuilds)
+        vtb_plan_destroy(p);
+        p = nullptr;
+        return r;
+    }
     return (L - 1) / 8 + 1;  // src/viterbiDecoderButterflyk1.c:256
 }
 

@@ -68,6 +68,15 @@ bool k7_global_supported(const Launch& a);
 size_t k7_global_workspace_bytes(const Launch& a);
 hipError_t launch_k7_global(const Launch& a);
 
+// K=7 single-frame latency path (k7_seg_kernel): one workgroup of up to 4 waves per frame,
+// the frame cut into up to 8 segments decoded at once (warm-up `warm` steps, a multiple of
+// 48), input staged through LDS (so it may sit in host-mapped memory), output written
+// directly, then *done (host-mapped, may be null) = 1, or 2 if a segment's metrics had not
+// converged (nothing written: decode the frame again with launch_k7_lds / _global).
+constexpr int kSegWarm = 96;
+bool k7_seg_supported(const Launch& a, int waves, int warm);
+hipError_t launch_k7_seg(const Launch& a, int waves, int warm, uint32_t* done);
+
 // K=7 streaming decode (vtb_stream_*, include/viterbi_amd.h): the global-survivor variant of
 // the K=7 kernel continued across launches.  All streams of one stream object advance in
 // lockstep, so the step counters are host-side; what depends on the data (how far each

@@ -573,8 +573,8 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
 // stream_traceback below).
 // Per phase: byte offset of the lane's (V, W) column in the table ring: its edge label c
 // and R = bit p of its location (the same for every frame pair of the wave).
-__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[6]) {
-    const int loc = int(lane_of(threadIdx.x));
+__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[6], int lane) {
+    const int loc = int(lane_of(uint32_t(lane)));
 #pragma unroll
     for (int ph = 0; ph < 6; ph++) {
         const int p = 5 - ph;
@@ -601,35 +601,57 @@ __device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, s
     }
 }
 
+// SEG (the single-frame latency path, k7_seg_kernel): one frame over the waves of one
+// workgroup, 2 segments per wave in the u16 halves.  Segment i runs sg.n steps from
+// g_i = i (n - warm); its decisions are the frame's from s_i = g_i + warm on (s_0 = 0) once
+// its metrics at s_i equal segment i-1's there up to a constant (checked after the ACS).
+struct SegArgs {
+    int n = 0;          // ACS steps per segment (multiple of 48)
+    int warm = 0;       // warm-up steps of segments 1.. (multiple of 48, < n)
+    int G = 0;          // segments in use (<= 2 x waves)
+    int seg_bytes = 0;  // LDS bytes per wave: table ring + survivor words (multiple of 256)
+    int in_lds = 0;     // LDS byte offset of the staged frame input
+    int x_lds = 0;      // LDS byte offset of the metric exchange area
+    uint32_t* done = nullptr;  // completion word: 1 decoded, 2 not converged (output not written)
+};
+
 // One frame pair (wave-pair index wp: frames 2wp, 2wp + 1); slot = this wave's survivor
 // workspace (GS).  pre: chunk 0's raw input is already in (pra, prb); next: the pair this wave
 // decodes after this one (its chunk 0 is prefetched into (pra, prb) before the traceback;
 // LDS variant only, whose traceback issues no global loads that would wait behind it).
 
-template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT, bool SEG = false>
 __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
                                         const StreamArgs& sa, size_t wp, size_t slot, bool pre, size_t next,
-                                        uint32_t& pra, uint32_t& prb, const uint32_t (&off)[6]) {
+                                        uint32_t& pra, uint32_t& prb, const uint32_t (&off)[6],
+                                        const SegArgs* sgp = nullptr, uint32_t* seg_out = nullptr) {
+    static_assert(!SEG || (SPLIT && !GS && !STREAM && !LOOP), "SEG runs the split pair on LDS survivors");
 
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
     using H = Hist<SOFT>;
     extern __shared__ uint4 smem4[];
-    uint8_t* smem = reinterpret_cast<uint8_t*>(smem4);
+    const int wv = SEG ? int(threadIdx.x >> 6) : 0;  // SEG: wave of the workgroup
+    uint8_t* smem = reinterpret_cast<uint8_t*>(smem4) + (SEG ? wv * sgp->seg_bytes : 0);
     uint8_t* tab = smem;
     uint32_t* dec = reinterpret_cast<uint32_t*>(smem + r0);
-    const int lane = threadIdx.x;
+    const int lane = SEG ? int(threadIdx.x & 63) : int(threadIdx.x);
     if (dbg & 16) return;  // measurement only: launch cost
     // SPLIT: one frame per wave, its two halves in the u16 halves of the registers: A = steps
     // [0, t1), B = steps [t1 - 96, T) (96 warm-up steps from equal start metrics).  If B's
     // metrics at t1 equal A's up to a constant, B's decisions from t1 on are the frame's
     // (the trellis only compares differences); otherwise the wave decodes the frame again
     // the normal way (pass 1).  Per-pass values:
-    const int t1s = SPLIT ? split_t1(T) : 0;
+    // SEG: wave wv runs segments 2wv (half A) and 2wv + 1 (half B; a copy of A if unused)
+    const int segA = 2 * wv, segB = SEG && 2 * wv + 1 < sgp->G ? 2 * wv + 1 : 2 * wv;
+    const int gA = SEG ? segA * (sgp->n - sgp->warm) : 0, gB = SEG ? segB * (sgp->n - sgp->warm) : 0;
+    const int warm = SEG ? sgp->warm : kSplitWarm;
+    const int t1s = SEG ? sgp->n : SPLIT ? split_t1(T) : 0;
     bool sp = SPLIT;                            // this pass runs split
-    int Tb = SPLIT ? T - t1s + kSplitWarm : T;  // frame B's steps (local)
+    int Tb = SEG ? T - gB : SPLIT ? T - t1s + kSplitWarm : T;  // frame B's steps (local)
+    const int Ta = SEG ? T - gA : T;                           // frame A's steps (local)
     const size_t fa = SPLIT ? wp : wp * 2, fb = fa + 1;
     const bool has_b = !SPLIT && fb < frames;
     const uint64_t gbase = (GS || STREAM) ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
@@ -642,7 +664,10 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // of the chunk before (so no compiler-placed use -- e.g. a zero-extension -- can pull
     // their wait up) and waited for where the chunk is staged, 36+ steps later.
     const int srow = lane < kChunk ? lane : lane - kChunk;  // staging row (lanes 48-63 duplicate 0-15)
-    // (wave-uniform frame bases in SGPRs, one 32-bit lane offset)
+    // (wave-uniform frame bases in SGPRs, one 32-bit lane offset; SEG: LDS byte addresses of
+    // the staged frame input)
+    const uint32_t ldsA = SEG ? uint32_t(sgp->in_lds + (SOFT ? 2 : 1) * gA) : 0u;
+    const uint32_t ldsB = SEG ? uint32_t(sgp->in_lds + (SOFT ? 2 : 1) * gB) : 0u;
     const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA));
     uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(inB));
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
@@ -662,6 +687,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             } else {
                 asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
                              : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            }
+        } else if constexpr (SEG) {
+            constexpr uint32_t SB = SOFT ? 2 : 1;
+            const uint32_t tca = ldsA + SB * uint32_t(t < Ta ? t : Ta - 1), tcb = ldsB + SB * uint32_t(t < Tb ? t : Tb - 1);
+            if constexpr (SOFT) {
+                asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(ra), "=&v"(rb) : "v"(tca), "v"(tcb));
+            } else {
+                asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %3" : "=&v"(ra), "=&v"(rb) : "v"(tca), "v"(tcb));
             }
         } else if constexpr (SPLIT) {
             constexpr uint32_t SB = SOFT ? 2 : 1;
@@ -689,7 +722,9 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #ifdef VTB_EXP_RAWNOWAIT
         ra = lane * 0x0101u, rb = lane * 0x0303u;  // measurement only: no wait for the loads
 #else
-        if (GS && !first) {
+        if constexpr (SEG) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
+        } else if (GS && !first) {
             asm volatile("s_waitcnt vmcnt(1)" : "+v"(ra), "+v"(rb));
         } else {
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
@@ -714,7 +749,8 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // Column k = c + 4R of the ring holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
     // (V, W) of a slot from two unrelated VGPRs by ds_write2_b32 (a ds_write_b64 would need
     // them in a register pair: 8 moves per chunk); three bases keep offsets below 256 dwords.
-    const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
+    // (LDS byte addresses: the ring starts at LDS address 0, SEG: at this wave's region)
+    const uint32_t wbase0 = uint32_t(SEG ? wv * sgp->seg_bytes : 0) + 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
     // PADCHK: the chunk may hold padding rows (only the chunk containing step T; the ACS
     // loop is split so that the check stays out of its other iterations).
     auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4], auto padchk) {
@@ -727,7 +763,21 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
 #undef VTB_W2
-        if (SPLIT && sp) {
+        if (SEG) {
+            // either half may hold padding rows (steps >= Ta in A, >= Tb in B): own-keeping rows
+            // there, as below
+            const int tr = c * kChunk + srow;
+            if (PADCHK && (tr >= Ta || tr >= Tb)) {
+                constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
+                const uint32_t keep = (tr >= Ta ? 0u : 0xFFFFu) | (tr >= Tb ? 0u : 0xFFFF0000u);
+                const uint32_t tie = et[0] - e[0];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    col[k * kCol] = make_uint2(e[k] & keep, (et[3 - k] & keep) | ((PADW + tie) & ~keep));
+                    col[(4 + k) * kCol] = make_uint2((et[k] & keep) | (tie & ~keep), (e[3 - k] & keep) | (PADW & ~keep));
+                }
+            }
+        } else if (SPLIT && sp) {
             // split pass: padding rows of frame B only (step >= Tb); frame A's half is real
             if (PADCHK && c * kChunk + srow >= Tb) {
                 constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1, LO = 0xFFFFu, HI = 0xFFFF0000u;
@@ -763,6 +813,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     }
     uint32_t M = (lane == 0) ? H::BIAS * kR1 : (H::BIAS + H::SC * INIT) * kR1;
     if (SPLIT && sp) M = (M & 0xFFFFu) | (H::BIAS << 16);  // frame B's half: equal start metrics
+    if (SEG && segA > 0) M = H::BIAS * kR1;                 // SEG: half A of waves 1.. too
     uint32_t msave = 0;                                      // (SPLIT) frame B's metrics at t1
     // first step of this launch: 0, or (streaming) where the previous call stopped
     const int tbeg = STREAM ? sa.t_begin : 0;
@@ -892,7 +943,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         for (int t0 = 0; t0 < tacs; t0 += kChunk) {
             prio(t0);
             acs_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
-            if (t0 == kSplitWarm - kChunk) msave = M;
+            if (t0 == warm - kChunk) msave = M;
         }
     } else {
         // chunks in order; only the one before the last stages padding rows
@@ -912,6 +963,10 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     __builtin_amdgcn_s_setprio(0);
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
     __syncthreads();
+    if constexpr (SEG) {  // the caller checks the segments and traces back
+        seg_out[0] = M, seg_out[1] = msave;
+        return;
+    }
     tstamp(table, 1);
     if constexpr (STREAM) {
         if (!sa.last) sa.state[wp * kStreamStateWords + lane] = M;
@@ -1040,7 +1095,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         tstamp(table, 0);
         clk0 = __builtin_amdgcn_s_memtime();
     }
-    column_offsets(table, off);
+    column_offsets(table, off, threadIdx.x);
     if constexpr (!LOOP) {
         k7_pair<SOFT, GS, STREAM, false, SPLIT>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
                                          ws_wave, sa, blockIdx.x, blockIdx.x, false, pairs, pra, prb, off);
@@ -1064,6 +1119,138 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
             table.tstamp[8 * blockIdx.x + 6] = hwid;
             table.tstamp[8 * blockIdx.x + 7] = xcc;
         }
+    }
+}
+
+// Single-frame latency path (SEG): one workgroup of W waves per frame, 2W segments of the
+// frame at once (one per u16 half; see SegArgs).  The frame's input is staged into LDS
+// first (a host-mapped frame crosses PCIe once, in one round trip), the segments' ACS run
+// in parallel, and segment i's metrics at s_i are checked against segment i - 1's (equal up
+// to a constant: every later decision of segment i is the frame's).  If every check holds,
+// wave 0 traces the frame back over all segments' survivor words (the frame decoder's
+// verified block-parallel chains, one chain of 48-step blocks over the 64 lanes) and writes
+// the bytes out; otherwise nothing is written and sg.done reports 2 (the caller decodes the
+// frame again with the frame kernel).  sg.done (host-mapped) is written last, after a
+// system-scope release, so a host thread can wait on it instead of synchronising the stream.
+constexpr int kSegLoads = 4;  // 16-byte staging loads per thread: frames of up to 64 B per thread
+template <bool SOFT>
+__global__ __launch_bounds__(256) void k7_seg_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
+                                                     int Tpad, int r0, int dbg, Launch table, SegArgs sg) {
+    extern __shared__ uint4 smem4[];
+    uint8_t* smem = reinterpret_cast<uint8_t*>(smem4);
+    const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63), W = int(blockDim.x >> 6);
+    // the frame's input bytes into LDS: up to four 16-byte loads per thread, all issued before
+    // any store (one round trip; the input buffer is padded to 16 bytes)
+    {
+        const uint8_t* src = in + size_t(blockIdx.x) * in_stride;
+        const int nin = (SOFT ? 2 : 1) * T;
+        uint4 v[kSegLoads];
+#pragma unroll
+        for (int j = 0; j < kSegLoads; j++) {
+            const int i = 16 * int(threadIdx.x + j * blockDim.x);
+            if (i < nin) v[j] = *reinterpret_cast<const uint4*>(src + i);
+        }
+#pragma unroll
+        for (int j = 0; j < kSegLoads; j++) {
+            const int i = 16 * int(threadIdx.x + j * blockDim.x);
+            if (i < nin) *reinterpret_cast<uint4*>(smem + sg.in_lds + i) = v[j];
+        }
+    }
+    __syncthreads();
+    uint32_t off[6];
+    column_offsets(table, off, lane);
+    uint32_t pra = 0, prb = 0, fm[2] = {0, 0};
+    k7_pair<SOFT, false, false, false, true, true>(in, in_stride, out, out_stride, T, L, Tpad, 0, r0, 1, dbg, table,
+                                                    nullptr, 0, StreamArgs(), blockIdx.x, blockIdx.x, false, 1, pra,
+                                                    prb, off, &sg, fm);
+    if (dbg & 16) return;
+    using H = Hist<SOFT>;
+    // exchange: final metrics (both halves) and the metrics at the end of the warm-up
+    uint32_t* xf = reinterpret_cast<uint32_t*>(smem + sg.x_lds);
+    uint32_t* xs = xf + 64 * W;
+    uint32_t* okw = xs + 64 * W;
+    xf[64 * wv + lane] = fm[0];
+    xs[64 * wv + lane] = fm[1];
+    __syncthreads();
+    constexpr uint32_t KEEP = 0xFFFFu & ~(H::SC - 1);
+    auto same_up_to_const = [](uint32_t a, uint32_t b) {  // a, b: this lane's metrics (history masked)
+        const uint32_t a0 = __builtin_amdgcn_readfirstlane(a), b0 = __builtin_amdgcn_readfirstlane(b);
+        return __ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) == ~0ull;
+    };
+    bool ok = true;
+    if (2 * wv + 1 < sg.G) ok = ok && same_up_to_const(fm[0] & KEEP, (fm[1] >> 16) & KEEP);  // half B vs half A
+    if (wv > 0) ok = ok && same_up_to_const((xf[64 * (wv - 1) + lane] >> 16) & KEEP, fm[1] & KEEP);  // A vs wave - 1's B
+    if (lane == 0) okw[wv] = ok ? 1u : 0u;
+    __syncthreads();
+    bool all = true;
+    for (int i = 0; i < W; i++) all = all && okw[i] != 0u;
+    if (wv != 0) return;  // (no barrier follows)
+    if (!all) {
+        if (sg.done && lane == 0) __hip_atomic_store(sg.done, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    // ---- traceback, wave 0: blocks of tbp steps (a multiple of 48), lane b = block b ----
+    const int step = sg.n - sg.warm;
+    auto col_at = [&](int tlo) -> uint32_t {  // survivor-word column of the 48 steps at tlo
+        int i = tlo < sg.warm ? 0 : (tlo - sg.warm) / step;
+        if (i > sg.G - 1) i = sg.G - 1;
+        const int lt = tlo - i * step;
+        return uint32_t((i >> 1) * sg.seg_bytes + r0 + 256 * (lt >> 4) + 2 * (i & 1));
+    };
+    auto tb48 = [&](uint32_t cb, uint32_t& l4) {
+        if constexpr (SOFT) return tb_body<false>(cb, l4, 0);
+        else return tb_body8<false>(cb, l4, 0);
+    };
+    uint8_t* ob = smem;  // decoded bytes (wave 0's table ring is free now), index t / 8
+    const int nb48 = Tpad / kChunk;
+    const int tbp = (nb48 + 63) / 64 * kChunk;
+    const bool active = lane * tbp < Tpad;
+    const int start_full = (lane + 1) * tbp + kTbWarm;
+    const int start = min(start_full, Tpad);
+    const bool known = start >= T;
+    const int nbody = (kTbWarm + tbp) / 48;
+    uint32_t loc = 0, loc_top = 0;
+    if (active) {
+        for (int g = 0; g < nbody; g++) {
+            const int tlo = start_full - 48 * (g + 1);
+            if (g == kTbWarm / 48) loc_top = loc;
+            if (tlo < start) {
+                const uint64_t bits = tb48(col_at(tlo), loc);
+                if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
+            }
+        }
+    }
+    uint32_t fin = loc;
+    bool fixed = known || !active;
+    for (int round = 0; round < 65; round++) {
+        const uint32_t sf = __shfl_down(fin, 1);
+        const bool okb = fixed || loc_top == sf;
+        const uint64_t bad = ~__ballot(okb);
+        if (bad == 0) break;
+        if (!okb && (bad >> (lane + 1)) == 0) {
+            loc = sf;
+            for (int g = kTbWarm / 48; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                put_bits48(ob, tlo, tb48(col_at(tlo), loc));
+            }
+            fin = loc;
+            fixed = true;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // copy out (bits past L are zero: the survivor ends in state 0)
+    const int nbytes = (L + 7) >> 3;
+    uint8_t* o = out + size_t(blockIdx.x) * out_stride;
+    if (((nbytes | size_t(o)) & 3) == 0) {
+        for (int i = lane; i < (nbytes >> 2); i += 64) reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(ob)[i];
+    } else {
+        for (int i = lane; i < nbytes; i += 64) o[i] = ob[i];
+    }
+    if (sg.done) {
+        __threadfence_system();
+        if (lane == 0) __hip_atomic_store(sg.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1147,6 +1334,56 @@ bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_
 size_t k7_global_workspace_bytes(const Launch& a) { return grid_waves<true>(a) * ws_wave_bytes(a.T); }
 
 hipError_t launch_k7_global(const Launch& a) { return launch_k7<true>(a); }
+
+// SEG geometry for a frame of T steps on W waves (warm-up `warm`): n = the ACS steps per
+// segment (multiple of 48) with 2W segments covering T, G = the segments whose exact region
+// [s_i, s_i+1) starts before T.
+bool k7_seg_geometry(int T, int W, int warm, SegArgs& sg) {
+    if (W < 1 || W > 4 || warm < 48 || warm % 48) return false;
+    const int G2 = 2 * W;
+    int n = (T + (G2 - 1) * warm + G2 - 1) / G2;
+    n = (n + kChunk - 1) / kChunk * kChunk;
+    if (n < warm + kChunk) n = warm + kChunk;
+    int G = 1;
+    while (G < G2 && G * (n - warm) + warm < T) G++;
+    if ((G - 1) * (n - warm) + n < T) return false;
+    sg.n = n, sg.warm = warm, sg.G = G;
+    return true;
+}
+
+bool k7_seg_supported(const Launch& a, int waves, int warm) {
+    SegArgs sg;
+    if (a.S != 6 || a.T < 240 || !k7_seg_geometry(a.T, waves, warm, sg)) return false;
+    const int W = (sg.G + 1) / 2, nin = (a.soft ? 2 : 1) * a.T;
+    const int r0 = (kRingBytes + 255) / 256 * 256;
+    const size_t lds = size_t(W) * (r0 + 16 * sg.n) + (nin + 15) / 16 * 16 + 4 * (2 * 64 * W + W);
+    return nin <= 16 * kSegLoads * 64 * W && lds <= 160 * 1024 && t_pad(a.T) / 8 + 8 <= r0;
+}
+
+hipError_t launch_k7_seg(const Launch& a, int waves, int warm, uint32_t* done) {
+    SegArgs sg;
+    if (!k7_seg_geometry(a.T, waves, warm, sg)) return hipErrorInvalidValue;
+    const int W = (sg.G + 1) / 2;  // waves in use
+    const int r0 = (kRingBytes + 255) / 256 * 256;
+    sg.seg_bytes = r0 + 16 * sg.n;
+    const int Tpad = t_pad(a.T);
+    const int nin = (a.soft ? 2 : 1) * a.T;  // staged bytes (the staging loads clamp to T - 1)
+    if (nin > 16 * kSegLoads * 64 * W) return hipErrorInvalidValue;
+    sg.in_lds = W * sg.seg_bytes;
+    sg.x_lds = sg.in_lds + (nin + 15) / 16 * 16;
+    sg.done = done;
+    const size_t lds = size_t(sg.x_lds) + 4 * (2 * 64 * W + W);
+    auto kern = a.soft ? k7_seg_kernel<true> : k7_seg_kernel<false>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           int(lds));
+        if (e != hipSuccess) return e;
+    }
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3(unsigned(a.frames)), dim3(64 * W), lds, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, Tpad, r0, debug_flags(), a, sg);
+    return hipGetLastError();
+}
 
 // One streaming call: every wave (two streams) continues its trellis over [s.t_begin,
 // s.t_end) and emits the final bits (stream_traceback).  LDS: the table ring only.

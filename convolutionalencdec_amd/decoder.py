@@ -146,6 +146,19 @@ class ViterbiDecoder:
             "vtb_decode_host")
         return out
 
+    def decode_frame(self, frame):
+        """One frame (host bytes in the plan's input layout) decoded synchronously at the lowest
+        latency (vtb_decode_frame_sync); returns ceil(L/8) bytes."""
+        x = np.ascontiguousarray(frame, dtype=np.uint8).reshape(-1)
+        if x.size != self.in_bytes:
+            raise ValueError(f"expected one frame of {self.in_bytes} bytes, got {x.size}")
+        out = np.zeros(self.out_bytes, np.uint8)
+        native.check(
+            native.lib().vtb_decode_frame_sync(self._plan, x.ctypes.data_as(ctypes.c_void_p),
+                                               out.ctypes.data_as(ctypes.c_void_p)),
+            "vtb_decode_frame_sync")
+        return out
+
     def decode(self, frames):
         try:
             import torch

@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "vtb_decode_host",
     "vtb_decode_host_multi",
     "vtb_release_cached_plans",
+    "vtb_decode_frame_sync",
     "vtb_decode_frame_legacy",
     "vtb_stream_create",
     "vtb_stream_destroy",
@@ -128,6 +129,7 @@ def lib():
     L.vtb_release_cached_plans.restype = None
     L.vtb_release_cached_plans.argtypes = []
     L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
+    L.vtb_decode_frame_sync.argtypes = [vp, vp, vp]
     L.vtb_stream_create.argtypes = [ctypes.POINTER(vp), cp, ctypes.c_int, sz, i32, ctypes.c_int]
     L.vtb_stream_destroy.restype = None
     L.vtb_stream_destroy.argtypes = [vp]
@@ -147,7 +149,7 @@ def lib():
     L.vtb_bsc_p32.argtypes = [ctypes.c_double]
     L.vtb_genk_decode_device.argtypes = [ctypes.POINTER(VtbGenKCode), i32, vp, sz, vp, sz, sz, vp]
     for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
-                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_stream_create", "vtb_stream_decode",
+                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_decode_frame_sync", "vtb_stream_create", "vtb_stream_decode",
                  "vtb_device_count", "vtb_payload_device",
                  "vtb_encode_device", "vtb_channel_device", "vtb_genk_decode_device"):
         getattr(L, name).restype = ctypes.c_int

@@ -14,6 +14,7 @@
  *   vtb_decode_host /       (one terminated frame per call with last=true, batched here
  *   vtb_decode_host_multi    over many frames; hard input is the reference byte-per-segment
  *                            layout; soft input is the build-defined 8-bit extension)
+ *   vtb_decode_frame_sync   the same, one frame from host memory, synchronous, lowest latency
  *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
  *                           behind include/viterbiDecoder.h (VITERBI_DECODER_HARD)
  *   vtb_legacy_metrics_k1   the metric update of a last=false call (:101-191), so the
@@ -125,6 +126,18 @@ int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
 
 /* Frees the plans vtb_decode_host_multi keeps.  Not concurrently with vtb_decode_host_multi. */
 void vtb_release_cached_plans(void);
+
+/* One frame from host memory to host memory, synchronously, at the lowest latency: the
+ * single-frame form of vtb_decode_host for callers that decode frame by frame (the legacy
+ * VITERBI_DECODER_HARD contract, one frame per call).  h_in holds one frame in the plan's
+ * input layout, h_out receives ceil(L/8) bytes.  K = 7 frames (T >= 240) are cut into up to
+ * eight segments decoded at once by the waves of one workgroup (each segment after the first
+ * starts 96 steps early from equal metrics and is used once its metrics provably match its
+ * predecessor's; otherwise the frame is decoded whole), reading the frame from and writing
+ * the bytes to plan-owned host-mapped memory, with completion signalled through host memory
+ * instead of a stream synchronisation.  Bit-exact with vtb_decode_host.  The plan's stream and
+ * buffers are used: one host thread per plan at a time. */
+int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out);
 
 /* One hard-input frame of `segments` coded segments from host memory (the legacy
  * VITERBI_DECODER_HARD contract).  Returns the reference's byte count

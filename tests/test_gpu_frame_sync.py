@@ -1,0 +1,125 @@
+"""GPU parity of the synchronous single-frame path (vtb_decode_frame_sync): K=7 frames cut
+into up to eight segments decoded at once by one workgroup (k7_seg_kernel), with the frame
+read from and the bytes written to host-mapped memory and completion signalled through host
+memory.  Every frame is compared bit for bit with the oracle / the reference's golden
+vectors; the path counters show that the segmented kernel decoded the clean and noisy frames
+and that unconverged segments (pure-noise input) fall back to the frame kernel."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import CODES, Oracle, golden_sets, hard_to_soft, random_frames
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import ConvCode, ViterbiDecoder, native  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+def seg_stats():
+    out = (ctypes.c_ulonglong * 3)()
+    native.lib().vtb_debug_seg_stats(out)
+    return np.array(list(out), np.int64)  # [seg decoded, seg not converged, no seg kernel]
+
+
+def run(dec, rx):
+    return np.stack([dec.decode_frame(r) for r in rx])
+
+
+def test_golden_vectors_k7(monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    s0 = seg_stats()
+    for key, L, unc, rx, decd in golden_sets(7):
+        for soft in (False, True):
+            d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L, soft=soft)
+            x = hard_to_soft(rx) if soft else rx
+            assert (run(d, x) == decd).all(), (key, soft)
+    s1 = seg_stats()
+    assert s1[0] > s0[0], (s0, s1)  # the segmented kernel ran (frames of T >= 240)
+
+
+@pytest.mark.parametrize("L", [234, 300, 1000, 1024, 2048, 2049, 3000, 4090, 8000])
+@pytest.mark.parametrize("soft", [False, True])
+def test_random_vs_oracle(orc, L, soft, monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    F = 6
+    if soft:
+        unc, rx = random_frames(orc, 7, L, F, 0.0, seed=L, soft=True, sigma=0.63)  # the bench's SNR
+    else:
+        unc, rx = random_frames(orc, 7, L, F, 0.05, seed=L)
+    want = orc.decode(7, CODES[7], rx, L, soft=soft)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L, soft=soft)
+    s0 = seg_stats()
+    got = run(d, rx)
+    s1 = seg_stats()
+    assert (got == want).all()
+    assert s1[0] - s0[0] >= F // 2, (s0, s1)  # these noise levels mostly converge within the warm-up
+
+
+@pytest.mark.parametrize("waves", [1, 2, 3])
+def test_fewer_waves(orc, waves, monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    monkeypatch.setenv("VTB_SEG_WAVES", str(waves))
+    L = 2048
+    unc, rx = random_frames(orc, 7, L, 4, 0.04, seed=waves)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L)
+    s0 = seg_stats()
+    assert (run(d, rx) == orc.decode(7, CODES[7], rx, L)).all()
+    assert seg_stats()[0] > s0[0]
+
+
+def test_pure_noise_falls_back(orc, monkeypatch):
+    """p = 0.5: segment metrics do not converge within 96 steps; the frame is decoded again by
+    the frame kernel, still bit-exact."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    L = 2048
+    unc, rx = random_frames(orc, 7, L, 8, 0.5, seed=5)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L)
+    s0 = seg_stats()
+    assert (run(d, rx) == orc.decode(7, CODES[7], rx, L)).all()
+    s1 = seg_stats()
+    assert s1[1] > s0[1]
+
+
+@pytest.mark.parametrize("K", [5, 9])
+def test_other_k_frame_kernel(orc, K, monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    L = 1000
+    unc, rx = random_frames(orc, K, L, 3, 0.03, seed=K)
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
+    s0 = seg_stats()
+    assert (run(d, rx) == orc.decode(K, CODES[K], rx, L)).all()
+    assert seg_stats()[2] - s0[2] == 3
+
+
+def test_short_frames(orc, monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    for L in (1, 8, 100, 233):
+        unc, rx = random_frames(orc, 7, L, 2, 0.05, seed=L)
+        d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L)
+        assert (run(d, rx) == orc.decode(7, CODES[7], rx, L)).all(), L
+
+
+def test_repeated_calls_one_plan(orc, monkeypatch):
+    """Back-to-back calls on one plan (the speedDecode loop): each call's bytes are its own."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    L = 2048
+    unc, rx = random_frames(orc, 7, L, 16, 0.02, seed=77)
+    want = orc.decode(7, CODES[7], rx, L)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L)
+    for rep in range(3):
+        for i in range(16):
+            assert (d.decode_frame(rx[i]) == want[i]).all(), (rep, i)
