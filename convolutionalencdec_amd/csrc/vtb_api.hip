@@ -529,7 +529,8 @@ int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
     std::vector<std::thread> th;
     for (size_t i = 0; i < G; i++) {
         // Contiguous shard [i*F/G, (i+1)*F/G): frames are independent, no collective.
-        size_t lo = frames * i / G, hi = frames * (i + 1) / G;
+        size_t lo = 0, hi = 0;
+        (void)vtb_shard_range(frames, G, i, &lo, &hi);
         th.emplace_back([&, i, lo, hi]() {
             if (hi <= lo) return;
             vtb_plan_t* p = nullptr;
@@ -562,6 +563,170 @@ int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
     return VTB_OK;
 }
 
+int vtb_shard_range(size_t frames, size_t shards, size_t index, size_t* lo, size_t* hi) {
+    if (!lo || !hi || shards == 0 || index >= shards) return VTB_ERR_INVALID;
+    // floor(F i / G) without overflowing F i (F < 2^64, G small): quotient and remainder parts
+    auto bound = [&](size_t i) { return (frames / shards) * i + (frames % shards) * i / shards; };
+    *lo = bound(index);
+    *hi = bound(index + 1);
+    return VTB_OK;
+}
+
+// vtb_decode_peer_multi's per-shard context: a stream and buffers on the shard's device, its
+// own plan (shards on one device run concurrently, and a plan's workspace belongs to one
+// stream), keyed by (device, occurrence of that device in the call's list).
+namespace {
+struct PeerCtx {
+    int device = -1, slot = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    size_t cap_in = 0, cap_out = 0;
+    vtb_plan_t* plan = nullptr;
+};
+std::mutex g_peer_mu;  // one vtb_decode_peer_multi call at a time (contexts are shared)
+std::vector<std::unique_ptr<PeerCtx>> g_peer;
+hipEvent_t g_peer_ready[64] = {};  // per source device: the caller's stream reached the call
+
+PeerCtx* peer_ctx(int dev, int slot) {
+    for (auto& c : g_peer)
+        if (c->device == dev && c->slot == slot) return c.get();
+    auto c = std::make_unique<PeerCtx>();
+    c->device = dev, c->slot = slot;
+    DeviceGuard g(dev);
+    if (!g.ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        return nullptr;
+    }
+    g_peer.push_back(std::move(c));
+    return g_peer.back().get();
+}
+
+bool grow(uint8_t*& p, size_t& cap, size_t need) {
+    if (need <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return false;
+    cap = need;
+    return true;
+}
+}  // namespace
+
+int vtb_decode_peer_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, int src_device,
+                          const uint8_t* d_in, uint8_t* d_out, size_t frames, const int* devices, int ndev,
+                          uint32_t flags, void* stream) {
+    int e = check_code(code);
+    if (e != VTB_OK) return e;
+    if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
+    if (frame_bits < 1 || !devices || ndev < 1 || ndev > 64 || (flags & ~uint32_t(VTB_PEER_STAGE_ALL)))
+        return VTB_ERR_INVALID;
+    if (frames == 0) return VTB_OK;
+    if (!d_in || !d_out) return VTB_ERR_INVALID;
+    if (frame_bits > VTB_MAX_FRAME_BITS) return VTB_ERR_UNSUPPORTED;
+    int nvis = 0;
+    if (hipGetDeviceCount(&nvis) != hipSuccess || src_device < 0 || src_device >= nvis || src_device >= 64 ||
+        !device_is_gfx950(src_device))
+        return VTB_ERR_DEVICE;
+    for (int i = 0; i < ndev; i++) {
+        const int d = devices[i];
+        if (d < 0 || d >= nvis || !device_is_gfx950(d)) return VTB_ERR_DEVICE;
+        if (d != src_device) {
+            // the shard crosses xGMI both ways: peer access in both directions or nothing
+            int a = 0, b = 0;
+            if (hipDeviceCanAccessPeer(&a, d, src_device) != hipSuccess ||
+                hipDeviceCanAccessPeer(&b, src_device, d) != hipSuccess || !a || !b)
+                return VTB_ERR_UNSUPPORTED;
+        }
+    }
+    const size_t ib = in_bytes(code, input, frame_bits), ob = out_bytes(frame_bits);
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    {
+        DeviceGuard g(src_device);
+        if (!g.ok) return VTB_ERR_DEVICE;
+        if (!g_peer_ready[src_device] &&
+            hipEventCreateWithFlags(&g_peer_ready[src_device], hipEventDisableTiming) != hipSuccess) {
+            g_peer_ready[src_device] = nullptr;
+            return VTB_ERR_DEVICE;
+        }
+        if (hipEventRecord(g_peer_ready[src_device], cs) != hipSuccess) return VTB_ERR_DEVICE;
+    }
+    std::vector<PeerCtx*> used;
+    int rc = VTB_OK;
+    for (int i = 0; i < ndev && rc == VTB_OK; i++) {
+        const int d = devices[i];
+        int slot = 0;
+        for (int j = 0; j < i; j++) slot += devices[j] == d ? 1 : 0;
+        size_t lo = 0, hi = 0;
+        (void)vtb_shard_range(frames, size_t(ndev), size_t(i), &lo, &hi);
+        if (hi <= lo) continue;
+        const size_t n = hi - lo;
+        PeerCtx* c = peer_ctx(d, slot);
+        if (!c) {
+            rc = VTB_ERR_DEVICE;
+            break;
+        }
+        DeviceGuard g(d);
+        if (!g.ok) {
+            rc = VTB_ERR_DEVICE;
+            break;
+        }
+        if (d != src_device) {
+            // enable both directions once (already-enabled is not an error)
+            hipError_t pe = hipDeviceEnablePeerAccess(src_device, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                rc = VTB_ERR_DEVICE;
+                break;
+            }
+            (void)hipGetLastError();
+            DeviceGuard gs(src_device);
+            pe = hipDeviceEnablePeerAccess(d, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                rc = VTB_ERR_DEVICE;
+                break;
+            }
+            (void)hipGetLastError();
+        }
+        if (!c->plan || c->plan->L != frame_bits || c->plan->input != input || !same_code(c->plan->code, *code)) {
+            vtb_plan_destroy(c->plan);
+            c->plan = nullptr;
+            if ((rc = vtb_plan_create(&c->plan, code, input, frame_bits, d)) != VTB_OK) {
+                c->plan = nullptr;
+                break;
+            }
+        }
+        if (hipStreamWaitEvent(c->stream, g_peer_ready[src_device], 0) != hipSuccess) {
+            rc = VTB_ERR_DEVICE;
+            break;
+        }
+        used.push_back(c);
+        if (d == src_device && !(flags & VTB_PEER_STAGE_ALL)) {
+            rc = launch(c->plan, d_in + lo * ib, ib, d_out + lo * ob, ob, n, c->stream);  // in place
+        } else {
+            if (!grow(c->in, c->cap_in, n * ib) || !grow(c->out, c->cap_out, n * ob)) {
+                rc = VTB_ERR_NOMEM;
+            } else if (hipMemcpyPeerAsync(c->in, d, d_in + lo * ib, src_device, n * ib, c->stream) != hipSuccess) {
+                rc = VTB_ERR_DEVICE;  // scatter (xGMI)
+            } else if ((rc = launch(c->plan, c->in, ib, c->out, ob, n, c->stream)) == VTB_OK &&
+                       hipMemcpyPeerAsync(d_out + lo * ob, src_device, c->out, d, n * ob, c->stream) != hipSuccess) {
+                rc = VTB_ERR_DEVICE;  // gather of the decoded bytes (xGMI)
+            }
+        }
+        if (hipEventRecord(c->done, c->stream) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
+    }
+    // the caller's stream waits for every shard (also after an error: queued copies still
+    // touch the caller's buffers)
+    DeviceGuard g(src_device);
+    for (PeerCtx* c : used)
+        if (hipStreamWaitEvent(cs, c->done, 0) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
+    if (rc != VTB_OK)
+        for (PeerCtx* c : used) (void)hipStreamSynchronize(c->stream);
+    return rc;
+}
+
 void vtb_release_cached_plans(void) {
     std::lock_guard<std::mutex> lk(g_plan_cache_mu);
     for (CachedPlan& c : g_plan_cache) {
@@ -569,6 +734,17 @@ void vtb_release_cached_plans(void) {
         vtb_plan_destroy(c.plan);
     }
     g_plan_cache.clear();
+    std::lock_guard<std::mutex> pk(g_peer_mu);
+    for (auto& c : g_peer) {
+        DeviceGuard g(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        vtb_plan_destroy(c->plan);
+        if (c->in) (void)hipFree(c->in);
+        if (c->out) (void)hipFree(c->out);
+        if (c->done) (void)hipEventDestroy(c->done);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    }
+    g_peer.clear();
 }
 
 int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t input, size_t streams,

@@ -256,6 +256,47 @@ def decode_multi(frames, code=ConvCode(), frame_bits=1024, soft=False, device_ma
     return out
 
 
+def shard_range(frames, shards, index):
+    """[lo, hi) of shard `index` of `shards` over `frames` frames (vtb_shard_range)."""
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    native.check(native.lib().vtb_shard_range(frames, shards, index, ctypes.byref(lo), ctypes.byref(hi)),
+                 "vtb_shard_range")
+    return lo.value, hi.value
+
+
+def decode_peer(frames, devices, code=ConvCode(), frame_bits=1024, soft=False, out=None, stage_all=False,
+                stream=None):
+    """Frames resident on one GPU (a torch uint8 tensor, rows of one frame) sharded across
+    `devices` peer to peer over xGMI (vtb_decode_peer_multi): shards on other GPUs are copied
+    there, decoded and their bytes copied back; the source GPU's own shard decodes in place.
+    Asynchronous on torch's current stream of the source device."""
+    import torch
+
+    code = code if isinstance(code, ConvCode) else ConvCode(*code)
+    T = frame_bits + code.S
+    ib = (2 if soft else 1) * T
+    x = frames.reshape(frames.shape[0], -1)
+    if frames.dtype != torch.uint8 or not frames.is_cuda or x.shape[1] != ib or not x.is_contiguous():
+        raise ValueError(f"frames must be a contiguous uint8 ROCm tensor of rows of {ib} bytes")
+    F = x.shape[0]
+    ob = (frame_bits + 7) // 8
+    if out is None:
+        out = torch.empty((F, ob), dtype=torch.uint8, device=frames.device)
+    elif out.dtype != torch.uint8 or out.device != frames.device or tuple(out.shape) != (F, ob) or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous uint8 [{F}, {ob}] tensor on {frames.device}")
+    if stream is None:
+        stream = torch.cuda.current_stream(frames.device).cuda_stream
+    devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+    c = code._c()
+    native.check(
+        native.lib().vtb_decode_peer_multi(ctypes.byref(c), native.VTB_INPUT_SOFT8 if soft else native.VTB_INPUT_HARD,
+                                           frame_bits, frames.device.index, ctypes.c_void_p(x.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), F, devs, len(devices),
+                                           native.VTB_PEER_STAGE_ALL if stage_all else 0, ctypes.c_void_p(stream)),
+        "vtb_decode_peer_multi")
+    return out
+
+
 class GenKDecoder:
     """Hard-decision decoder for a rate-k/n code (k input bits per trellis step), the
     reference's generic `viterbiDecoderHard` (src/viterbiDecoder.c:52-234) as terminated

@@ -18,6 +18,8 @@ VTB_ERR_UNSUPPORTED = -3
 VTB_ERR_DEVICE = -4
 VTB_ERR_NOMEM = -5
 
+VTB_PEER_STAGE_ALL = 1
+
 VTB_INPUT_HARD = 0
 VTB_INPUT_SOFT8 = 1
 
@@ -36,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "vtb_decode_host",
     "vtb_decode_host_multi",
     "vtb_release_cached_plans",
+    "vtb_shard_range",
+    "vtb_decode_peer_multi",
     "vtb_decode_frame_sync",
     "vtb_decode_frame_legacy",
     "vtb_stream_create",
@@ -128,6 +132,9 @@ def lib():
     L.vtb_decode_host_multi.argtypes = [cp, ctypes.c_int, i32, vp, vp, sz, ctypes.c_uint32]
     L.vtb_release_cached_plans.restype = None
     L.vtb_release_cached_plans.argtypes = []
+    L.vtb_shard_range.argtypes = [sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    L.vtb_decode_peer_multi.argtypes = [cp, ctypes.c_int, i32, ctypes.c_int, vp, vp, sz, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.c_int, ctypes.c_uint32, vp]
     L.vtb_decode_frame_legacy.argtypes = [cp, vp, i32, vp]
     L.vtb_decode_frame_sync.argtypes = [vp, vp, vp]
     L.vtb_stream_create.argtypes = [ctypes.POINTER(vp), cp, ctypes.c_int, sz, i32, ctypes.c_int]
@@ -149,7 +156,7 @@ def lib():
     L.vtb_bsc_p32.argtypes = [ctypes.c_double]
     L.vtb_genk_decode_device.argtypes = [ctypes.POINTER(VtbGenKCode), i32, vp, sz, vp, sz, sz, vp]
     for name in ("vtb_code_check", "vtb_edge_table", "vtb_plan_create", "vtb_decode_device", "vtb_decode_host",
-                 "vtb_decode_host_multi", "vtb_decode_frame_legacy", "vtb_decode_frame_sync", "vtb_stream_create", "vtb_stream_decode",
+                 "vtb_decode_host_multi", "vtb_decode_peer_multi", "vtb_shard_range", "vtb_decode_frame_legacy", "vtb_decode_frame_sync", "vtb_stream_create", "vtb_stream_decode",
                  "vtb_device_count", "vtb_payload_device",
                  "vtb_encode_device", "vtb_channel_device", "vtb_genk_decode_device"):
         getattr(L, name).restype = ctypes.c_int

@@ -12,7 +12,8 @@
  *   vtb_edge_table          viterbiInitButterflyk1        src/viterbiDecoderButterflyk1.c:8-44
  *   vtb_decode_device /     viterbiDecoderHardButterflyk1 src/viterbiDecoderButterflyk1.c:82-263
  *   vtb_decode_host /       (one terminated frame per call with last=true, batched here
- *   vtb_decode_host_multi    over many frames; hard input is the reference byte-per-segment
+ *   vtb_decode_host_multi /  over many frames; hard input is the reference byte-per-segment
+ *   vtb_decode_peer_multi
  *                            layout; soft input is the build-defined 8-bit extension)
  *   vtb_decode_frame_sync   the same, one frame from host memory, synchronous, lowest latency
  *   vtb_decode_frame_legacy the same, one frame from host memory, for the legacy shim
@@ -124,8 +125,31 @@ int vtb_decode_host(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out, size_
 int vtb_decode_host_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, const uint8_t* h_in,
                           uint8_t* h_out, size_t frames, uint32_t device_mask);
 
-/* Frees the plans vtb_decode_host_multi keeps.  Not concurrently with vtb_decode_host_multi. */
+/* Frees the plans vtb_decode_host_multi keeps and vtb_decode_peer_multi's per-device
+ * contexts.  Not concurrently with either. */
 void vtb_release_cached_plans(void);
+
+/* Shard i of `shards` over `frames` frames: [*lo, *hi) = [floor(F i / G), floor(F (i+1) / G)),
+ * contiguous, tiling [0, F), sizes differing by at most one.  The split every multi-GPU entry
+ * point uses. */
+int vtb_shard_range(size_t frames, size_t shards, size_t index, size_t* lo, size_t* hi);
+
+/* Device-sourced sharding over xGMI (SURVEY.md §8 e, BASELINE config C5 fed from one GPU):
+ * `frames` packed frames resident on src_device (d_in, d_out are device pointers there) are
+ * split into ndev contiguous shards (vtb_shard_range), shard i decoded on devices[i]: a shard
+ * on another GPU is copied there peer to peer (hipMemcpyPeerAsync over xGMI), decoded, and
+ * its ceil(L/8)-byte rows copied back into d_out; a shard on src_device is decoded in place
+ * (flags VTB_PEER_STAGE_ALL: staged through its own buffers like a peer shard -- testing and
+ * A/B on one GPU).  A device may be listed more than once (one shard per entry).
+ * Asynchronous on `stream` (a hipStream_t of src_device): the shards start after the work
+ * queued there and `stream` waits for all of them.  VTB_ERR_UNSUPPORTED if a listed device
+ * and src_device cannot access each other as peers (peer access is enabled on first use).
+ * Per-(device, entry) streams, plans and buffers are kept for later calls
+ * (vtb_release_cached_plans frees them); one call at a time. */
+#define VTB_PEER_STAGE_ALL 1u
+int vtb_decode_peer_multi(const vtb_code_t* code, vtb_input_t input, int32_t frame_bits, int src_device,
+                          const uint8_t* d_in, uint8_t* d_out, size_t frames, const int* devices, int ndev,
+                          uint32_t flags, void* stream);
 
 /* One frame from host memory to host memory, synchronously, at the lowest latency: the
  * single-frame form of vtb_decode_host for callers that decode frame by frame (the legacy

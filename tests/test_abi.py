@@ -100,3 +100,37 @@ def test_plan_without_gpu_fails_loudly():
     assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(c), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
     k9 = native.VtbCode.make(9, CODES[9])
     assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k9), 0, 8, 0, 0) == native.VTB_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("F", [0, 1, 2, 3, 7, 100, 1001, 4096, 131072, 2**20, 2**20 + 5, 2**40 + 3])
+def test_shard_range_tiles_the_batch(F):
+    """The frame split of vtb_decode_host_multi / vtb_decode_peer_multi: contiguous shards that
+    tile [0, F) exactly, sizes differing by at most one, for even and uneven F / G."""
+    from convolutionalencdec_amd import shard_range
+
+    for G in (1, 2, 3, 4, 5, 7, 8, 9, 16, 64):
+        bounds = [shard_range(F, G, i) for i in range(G)]
+        assert bounds[0][0] == 0 and bounds[-1][1] == F
+        assert all(bounds[i][1] == bounds[i + 1][0] for i in range(G - 1))
+        sizes = [hi - lo for lo, hi in bounds]
+        assert min(sizes) >= 0 and max(sizes) - min(sizes) <= 1
+        assert sum(sizes) == F
+
+
+def test_shard_range_and_peer_multi_argument_errors():
+    lib = native.lib()
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    assert lib.vtb_shard_range(10, 0, 0, ctypes.byref(lo), ctypes.byref(hi)) == native.VTB_ERR_INVALID
+    assert lib.vtb_shard_range(10, 4, 4, ctypes.byref(lo), ctypes.byref(hi)) == native.VTB_ERR_INVALID
+    assert lib.vtb_shard_range(10, 4, 0, None, ctypes.byref(hi)) == native.VTB_ERR_INVALID
+    c = native.VtbCode.make(7, CODES[7])
+    devs = (ctypes.c_int * 2)(0, 0)
+    buf = ctypes.c_void_p(0x1000)
+    args = (ctypes.byref(c), 0, 1024, 0, buf, buf, 16)
+    assert lib.vtb_decode_peer_multi(*args, devs, 0, 0, None) == native.VTB_ERR_INVALID  # no devices
+    assert lib.vtb_decode_peer_multi(*args, devs, 2, 0x80, None) == native.VTB_ERR_INVALID  # unknown flag
+    bad = native.VtbCode.make(7, (0o112, 0o171))
+    assert lib.vtb_decode_peer_multi(ctypes.byref(bad), 0, 1024, 0, buf, buf, 16, devs, 2, 0,
+                                     None) == native.VTB_ERR_CODE
+    if lib.vtb_device_count() == 0:  # no GPU here: the device check fails loudly
+        assert lib.vtb_decode_peer_multi(*args, devs, 2, 0, None) == native.VTB_ERR_DEVICE
