@@ -33,6 +33,7 @@ sys.path.insert(0, REPO)
 METRIC = "decoded info Mbit/s, K=7 r=1/2 soft-dec, batch 4096 frames @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 K, G = 7, (0o113, 0o171)
+CODES = {5: (5, (0o23, 0o35)), 7: (7, G), 9: (9, (0o561, 0o753))}
 
 
 def parse():
@@ -213,11 +214,12 @@ def stream_bench(args, dev, local, world):
     F, C, soft = args.frames, args.stream_chunk, not args.hard
     steps, warm = args.steps, args.warmup
     L = (steps + warm) * C
-    d_unc, d_rx = devframes.make_frames(ConvCode(*(K, G)), F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
+    code = ConvCode(*CODES[args.K])
+    d_unc, d_rx = devframes.make_frames(code, F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
                                         seed=shard_seed(int(os.environ.get("RANK", "0"))), device=local)
     sb = 2 if soft else 1
     x = d_rx.reshape(F, -1)
-    vs = ViterbiStream(ConvCode(K, G), streams=F, soft=soft, window_steps=max(4 * C, 4096), device=local)
+    vs = ViterbiStream(code, streams=F, soft=soft, window_steps=max(4 * C, 4096), device=local)
     outs = []
 
     def push(i, last=False):
@@ -249,7 +251,7 @@ def stream_bench(args, dev, local, world):
     line = {"metric": METRIC, "value": round(value, 2), "unit": "Mbit/s", "n_gpus": 1, "steps": steps, "warmup": warm,
             "ms_per_step": round(dt / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u16", "data": "synthetic (device generator)",
-            "config": {"workload": f"streaming K=7 r=1/2 {'8-bit soft' if soft else 'hard'}-decision, {F} streams x "
+            "config": {"workload": f"streaming K={args.K} r=1/2 {'8-bit soft' if soft else 'hard'}-decision, {F} streams x "
                                    f"{C} segments per call (vtb_stream_decode), one {L}-bit frame per stream",
                        "streams": F, "segments_per_call": C, "decoded_ber_first8": ber},
             "roofline": {"bound": "hbm", "achieved": round(alg / (call_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
@@ -294,7 +296,7 @@ def main():
 
     from convolutionalencdec_amd import ConvCode, ViterbiDecoder, synth
 
-    code = (K, G) if args.K == 7 else (args.K, {5: (0o23, 0o35), 9: (0o561, 0o753)}[args.K])
+    code = CODES[args.K]
     soft = not args.hard
     F, L = args.frames, args.frame_bits
     T = L + code[0] - 1

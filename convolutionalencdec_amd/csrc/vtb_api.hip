@@ -753,11 +753,14 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     *sp = nullptr;
     int e = check_code(code);
     if (e != VTB_OK) return e;
-    if (code->constraint_length != 7) return VTB_ERR_UNSUPPORTED;
+    if (code->constraint_length != 7 && code->constraint_length != 9) return VTB_ERR_UNSUPPORTED;
+    const bool k9 = code->constraint_length == 9;
     if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
     if (streams == 0 || streams > (size_t(1) << 31)) return VTB_ERR_INVALID;
-    const int64_t win = window_steps <= 0 ? 49152 : (int64_t(window_steps) + 47) / 48 * 48;
-    if (win < 96 || win > (int64_t(1) << 27)) return VTB_ERR_INVALID;  // 16 B per step: 32-bit ring offsets
+    // default window: 49,152 steps (K = 7, 768 KB per wave) / 12,288 (K = 9, 64 B per step:
+    // the same 768 KB; K = 9 survivor paths merge within a few hundred steps at useful SNR)
+    const int64_t win = window_steps <= 0 ? (k9 ? 12288 : 49152) : (int64_t(window_steps) + 47) / 48 * 48;
+    if (win < 96 || win > (int64_t(1) << (k9 ? 25 : 27))) return VTB_ERR_INVALID;  // 32-bit ring offsets
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return VTB_ERR_DEVICE;
     if (!device_is_gfx950(device)) return VTB_ERR_DEVICE;
@@ -772,13 +775,14 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     s->device = device;
     edge_table(code, s->symm);
     const size_t waves = (streams + 1) / 2;
-    if (hipMalloc(&s->d_state, waves * vtb::kStreamStateWords * 4) != hipSuccess ||
+    const size_t sw = k9 ? vtb::kStreamStateWords9 : vtb::kStreamStateWords, step_bytes = k9 ? 64 : 16;
+    if (hipMalloc(&s->d_state, waves * sw * 4) != hipSuccess ||
         hipMalloc(&s->d_carry, streams * vtb::kStreamCarryStride) != hipSuccess ||
-        hipMalloc(&s->d_ring, waves * 16 * size_t(s->ring)) != hipSuccess) {
+        hipMalloc(&s->d_ring, waves * step_bytes * size_t(s->ring)) != hipSuccess) {
         vtb_stream_destroy(s);
         return VTB_ERR_NOMEM;
     }
-    if (hipMemset(s->d_state, 0, waves * vtb::kStreamStateWords * 4) != hipSuccess) {
+    if (hipMemset(s->d_state, 0, waves * sw * 4) != hipSuccess) {
         vtb_stream_destroy(s);
         return VTB_ERR_DEVICE;
     }
@@ -840,7 +844,7 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
         sa.last = last ? 1 : 0;
         sa.ring = s->ring;
         sa.out_bits = d_out_bits;
-        if (vtb::launch_k7_stream(a, sa) != hipSuccess) return VTB_ERR_DEVICE;
+        if ((a.S == 8 ? vtb::launch_k9_stream(a, sa) : vtb::launch_k7_stream(a, sa)) != hipSuccess) return VTB_ERR_DEVICE;
     }
     // rows received past the last whole 48-step chunk wait in the carry for the next call
     const int leftover = last ? 0 : rows - nproc;

@@ -96,6 +96,10 @@ struct StreamArgs {
     int32_t* out_bits = nullptr;     // per stream: bits emitted by this call, -1 = window overflow
 };
 hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s);
+// K = 9 (vtb_k9.hip): the same protocol, 4 metric registers per lane, 64 B of survivor words
+// per step and wave in the ring.
+constexpr int kStreamStateWords9 = 260;  // per wave: M[4][64], e[2], flags, pad
+hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s);
 
 // K=9, survivors in a global workspace (vtb_k9.hip).
 bool k9_supported(const Launch& a);

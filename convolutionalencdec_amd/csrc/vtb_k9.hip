@@ -240,6 +240,162 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
     o[2] = (unsigned short)((rh >> 24) | ((rh >> 8) & 0xff00u));
 }
 
+// Decoded bits of steps [tlo, tlo + 48) to global memory at o (byte stores: a stream row has
+// no alignment guarantee).
+__device__ __forceinline__ void put_bits48_global(uint8_t* o, uint64_t bits) {
+    const uint32_t r = __builtin_bitreverse32(uint32_t(bits)), rh = __builtin_bitreverse32(uint32_t(bits >> 32));
+    o[0] = uint8_t(r >> 24), o[1] = uint8_t(r >> 16), o[2] = uint8_t(r >> 8), o[3] = uint8_t(r);
+    o[4] = uint8_t(rh >> 24), o[5] = uint8_t(rh >> 16);
+}
+
+// Eight survivor walks of 48 steps each (the location part of tb_body / tb_body8 only), all
+// eight loads of a window issued before one wait: the streaming merge test walks all 256 end
+// locations of a frame, eight per lane, and each walk is a chain of dependent loads.
+template <bool SOFT>
+__device__ __forceinline__ void tb_walk48_x8(uint32_t cb, uint32_t (&la)[8], uint64_t gbase) {
+    uint32_t a[8], v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = cb | la[k];
+    if constexpr (SOFT) {
+#pragma unroll
+        for (int j = 0; j < 24; j++) {
+            const int todd = 47 - 2 * j;
+            const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                asm volatile("global_load_ushort %0, %1, %2 offset:%3" : "=v"(v[k]) : "v"(a[k]), "s"(gbase),
+                             "i"((todd >> 4) * kColBytes));
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                         "+v"(v[6]), "+v"(v[7]));
+            const int pos = addr_pos((todd - 1) & 7);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t fld = pos >= sh ? (v[k] << (pos - sh)) : (v[k] >> (sh - pos));
+                a[k] = (a[k] & ~(3u << pos)) | (fld & (3u << pos));
+            }
+        }
+    } else {
+#pragma unroll
+        for (int o = 5; o >= 0; o--) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                asm volatile("global_load_ubyte %0, %1, %2 offset:%3" : "=v"(v[k]) : "v"(a[k]), "s"(gbase),
+                             "i"(kColBytes * (o >> 1) + (o & 1)));
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                         "+v"(v[6]), "+v"(v[7]));
+#pragma unroll
+            for (int k = 0; k < 8; k++) a[k] = (a[k] & ~0x3FCu) | (v[k] & 0xFCu) | ((v[k] & 3u) << 8);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) la[k] = a[k] & 0x3FCu;
+}
+
+// Traceback of one streaming call (vtb_stream_decode, K = 9): vtb_k7_lds.hip
+// stream_traceback with 256 locations.  Frame f of the wave (lanes 32f .. 32f + 31) has
+// emitted the bits of steps [0, e_f) before the call.
+//  * Not last: walks from all 256 locations at t_end (eight per lane) go back 48 steps at a
+//    time until they stand on one location (step m): no later input can change the path
+//    below m, so the bits of [e_f, m) equal the whole-frame decode's and are emitted.
+//    m <= t_end - 48, so the zero tail is never emitted early.
+//  * Last: the terminated traceback from location 0 at T (the padding steps keep location 0)
+//    emits [e_f, T - 8).
+// The emission is the frame decoder's verified block-parallel traceback, 32 blocks per frame.
+// If the ring no longer holds step e_f (no merge within sa.ring steps) the frame is flagged:
+// -1 bits until last.
+template <bool SOFT>
+__device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
+                                  uint64_t gbase, size_t fa, bool has_b, size_t wp) {
+    const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
+    uint32_t* st = sa.state + wp * kStreamStateWords9;
+    const int e0 = int(st[256 + f]);
+    const uint32_t flags0 = __builtin_amdgcn_readfirstlane(st[258]);
+    const bool real = f == 0 || has_b;
+    const bool lost = ((flags0 >> f) & 1u) || t_end - e0 > sa.ring;
+    auto colb = [&](int tlo) { return uint32_t(2 * f + kColBytes * ((tlo % sa.ring) >> 4)); };
+    auto tb48 = [&](int tlo, uint32_t& la) -> uint64_t {
+        if constexpr (SOFT) return tb_body(colb(tlo), la, gbase);
+        else return tb_body8(colb(tlo), la, gbase);
+    };
+    int hi = e0, kfrom = e0;
+    uint32_t kloc = 0;
+    if (sa.last) {
+        hi = t_end, kfrom = T;
+    } else {
+        // merge test: lane j of frame f walks the locations l' = j + 32 k, k = 0..7
+        uint32_t la[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t lp = uint32_t(blk + 32 * k);
+            la[k] = (lp & 0xFCu) | ((lp & 3u) << 8);
+        }
+        bool walking = !lost && real;
+        for (int tlo = t_end - 48; __builtin_amdgcn_readfirstlane(__ballot(walking && tlo >= e0) != 0); tlo -= 48) {
+            const bool here = walking && tlo >= e0;
+            if (here) tb_walk48_x8<SOFT>(colb(tlo), la, gbase);
+            const uint32_t ref = __shfl(la[0], 32 * f);
+            bool all = true;
+#pragma unroll
+            for (int k = 0; k < 8; k++) all = all && la[k] == ref;
+            const uint64_t same = __ballot(all);
+            const bool merged = uint32_t(same >> (32 * f)) == 0xFFFFFFFFu;
+            if (here && merged) {
+                hi = kfrom = tlo, kloc = ref;
+                walking = false;
+            }
+            if (tlo < e0) walking = false;
+        }
+    }
+    if (!lost && real && hi > e0) {
+        const int n = hi - e0;                           // multiple of 48
+        const int tbb = ((n + 31) / 32 + 47) / 48 * 48;  // 32 blocks per frame
+        const int bot = e0 + blk * tbb;
+        const bool active = bot < hi;
+        const int start_full = bot + tbb + kTbWarm;
+        const int start = min(start_full, hi);
+        const bool known = start >= kfrom;
+        const int nbody = (kTbWarm + tbb) / 48;
+        uint8_t* ob = out + (fa + f) * out_stride;  // byte (tlo - e0) / 8 of the call's bits
+        uint32_t loc = known ? kloc : 0u, loc_top = loc;
+        if (active) {
+            for (int g = 0; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                if (g == kTbWarm / 48) loc_top = loc;
+                if (tlo < start) {
+                    const uint64_t bits = tb48(tlo, loc);
+                    if (g >= kTbWarm / 48) put_bits48_global(ob + ((tlo - e0) >> 3), bits);
+                }
+            }
+        }
+        uint32_t fin = loc;
+        bool fixed = known || !active;
+        for (int round = 0; round < 33; round++) {
+            const uint32_t sf = __shfl_down(fin, 1);
+            const bool ok = fixed || loc_top == sf;
+            const uint64_t bad = ~__ballot(ok);
+            const uint32_t badf = uint32_t(bad >> (32 * f));
+            if (badf == 0 && uint32_t(bad >> (32 * (1 - f))) == 0) break;
+            const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
+            if (!ok && succ_proven) {
+                loc = sf;
+                for (int g = kTbWarm / 48; g < nbody; g++) {
+                    const int tlo = start_full - 48 * (g + 1);
+                    put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, loc));
+                }
+                fin = loc;
+                fixed = true;
+            }
+        }
+    }
+    const int bits_out = lost ? -1 : sa.last ? T - 8 - e0 : hi - e0;
+    if (real && blk == 0) sa.out_bits[fa + f] = bits_out;
+    const uint64_t lostmask = __ballot(lost && real && blk == 0);
+    const uint32_t flags = sa.last ? 0u : uint32_t((lostmask & 1u) | ((lostmask >> 32) & 1u) << 1);
+    const int e_next = sa.last || lost ? (sa.last ? 0 : e0) : hi;
+    if (blk == 0) st[256 + f] = uint32_t(e_next);
+    if (lane == 0) st[258] = flags;
+}
+
 // Per register and phase: byte offset of the (V, W) column (edge label c of the butterfly's
 // upper state, R = bit p of the location); the same for every frame pair of the wave.
 __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[4][8]) {
@@ -255,11 +411,15 @@ __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&o
 
 // One frame pair (wave-pair index wp: frames 2wp, 2wp + 1), survivors in workspace slot
 // `slot` (this wave's).
-template <bool SOFT>
+// STREAM: one call of the streaming decoder (vtb_stream_decode): steps [sa.t_begin, Tpad =
+// sa.t_end) continue from the metrics in sa.state (delta = 0, Tq = T = the steps received so
+// far), survivor words go to a ring of sa.ring steps (ws_wave = 64 sa.ring bytes per wave), and
+// stream_traceback9 emits the bits that became final.
+template <bool SOFT, bool STREAM = false>
 __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
                                         size_t frames, int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t wp,
-                                        size_t slot, const uint32_t (&off)[4][8]) {
+                                        size_t slot, const uint32_t (&off)[4][8], const StreamArgs& sa = StreamArgs()) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
     using H = Hist<SOFT>;
     constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
@@ -280,7 +440,21 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         int t = c * kCh + srow - delta;
         t = t < 0 ? 0 : (t < T ? t : T - 1);
-        if constexpr (SOFT) {
+        if constexpr (STREAM) {
+            // row r of this call: the carry's held-back rows first, then the new input
+            constexpr int SB = SOFT ? 2 : 1;
+            const int r = t - sa.t_begin;
+            const uint8_t* pa = r < sa.carry_len ? sa.carry + fa * kStreamCarryStride + SB * r : inA + SB * (r - sa.carry_len);
+            const uint8_t* pb = r < sa.carry_len ? sa.carry + (has_b ? fb : fa) * kStreamCarryStride + SB * r
+                                                 : inB + SB * (r - sa.carry_len);
+            if constexpr (SOFT) {
+                asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off"
+                             : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            } else {
+                asm volatile("global_load_ubyte %0, %2, off\n\tglobal_load_ubyte %1, %3, off"
+                             : "=&v"(ra), "=&v"(rb) : "v"(pa), "v"(pb));
+            }
+        } else if constexpr (SOFT) {
             asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
                          : "=&v"(ra), "=&v"(rb) : "v"(2u * uint32_t(t)), "s"(baseA), "s"(baseB));
         } else {
@@ -333,13 +507,19 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t M[4];
     M[0] = (lane == 0) ? B4 * kR1 : (B4 + H::SC * Q) * kR1;
     M[1] = M[2] = M[3] = (B4 + H::SC * Q) * kR1;
+    const int tbeg = STREAM ? sa.t_begin : 0;  // first step of this launch
+    if constexpr (STREAM) {
+        if (tbeg > 0)
+#pragma unroll
+            for (int r = 0; r < 4; r++) M[r] = sa.state[wp * kStreamStateWords9 + 64 * r + lane];
+    }
     uint32_t ra, rb;
-    {
+    if (!STREAM || Tpad > tbeg) {
         uint32_t e[4], et[4];
-        load_raw(0, ra, rb);
+        load_raw(tbeg / kCh, ra, rb);
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
         stage_compute(ra, rb, e, et);
-        stage_write(0, e, et);
+        stage_write(tbeg / kCh, e, et);
     }
     uint2 buf[kRS][4];
 #pragma unroll
@@ -350,9 +530,10 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     const uint32_t wlane = 4u * rev6(lam);  // survivor word byte offset of the lane within a column
     uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4];
     const int tacs = (dbg & 2) ? 0 : Tpad;
-    for (int t0 = 0; t0 < tacs; t0 += kCh) {
+    for (int t0 = tbeg; t0 < tacs; t0 += kCh) {
         const int c0 = t0 / kCh;
-        const uint32_t gvo = uint32_t(kColBytes) * uint32_t(t0 >> 4) + wlane;
+        // survivor column of step t0 (streaming: position in the ring)
+        const uint32_t gvo = uint32_t(kColBytes) * uint32_t((STREAM ? t0 % sa.ring : t0) >> 4) + wlane;
         static_for(std::make_integer_sequence<int, kCh>{}, [&](auto ic) {
             constexpr int I = decltype(ic)::value;
             constexpr int PH = I % 8;
@@ -424,6 +605,37 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+    if constexpr (STREAM) {
+        if (!sa.last)
+#pragma unroll
+            for (int r = 0; r < 4; r++) sa.state[wp * kStreamStateWords9 + 64 * r + lane] = M[r];
+        // Soft input, last call, padding steps [T, Tpad): own-keeping survivor bits, one bit per
+        // step (T may be odd: the window of step T - 1 keeps its real even-step bit)
+        if (SOFT && sa.last) {
+            uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + slot * ws_wave);
+            for (int g = T >> 4; g < (Tpad >> 4); g++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t lp = (rev6(lam) << 2) | uint32_t(rev2(r));
+                    uint32_t own = 0, mask = 0;
+                    for (int t = (16 * g > T ? 16 * g : T); t < 16 * g + 16; t++) {
+                        const int w = (t & 15) >> 1, bit = 8 * (w & 1) + 2 * (w >> 1) + (t & 1);
+                        own |= ((lp >> (t & 7)) & 1u) << bit;
+                        mask |= 1u << bit;
+                    }
+                    own |= own << 16;
+                    mask |= mask << 16;
+                    uint32_t* p = wsw + (kColBytes / 4) * ((16 * g % sa.ring) >> 4) + (wlane >> 2) + 64 * rev2(r);
+                    *p = (*p & ~mask) | (own & mask);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (dbg & 1) return;
+        stream_traceback9<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp);
+        return;
+    }
     // Soft input, padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping
     // decisions (both history bits = the location's own bits t_even mod 8, +1 of l').
     if (SOFT && !(dbg & 2)) {
@@ -506,14 +718,18 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
 
 // LOOP: persistent over frame pairs (as vtb_k7_lds.hip), wave b decodes pairs b, b + grid, ...;
 // !LOOP: one wave per pair, for batches the CUs hold in one round (fewer live registers).
-template <bool SOFT, bool LOOP>
+template <bool SOFT, bool LOOP, bool STREAM = false>
 __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                 uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
                                                 int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
-                                                uint8_t* __restrict__ ws, size_t ws_wave) {
+                                                uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa = StreamArgs()) {
+    static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
     uint32_t off[4][8];
     column_offsets(table, off);
-    if constexpr (!LOOP) {
+    if constexpr (STREAM) {
+        k9_pair<SOFT, true>(in, in_stride, out, out_stride, T, L, 0, T, Tpad, 0, frames, dbg, ws, ws_wave, blockIdx.x,
+                            blockIdx.x, off, sa);
+    } else if constexpr (!LOOP) {
         k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, blockIdx.x,
                       blockIdx.x, off);
     } else {
@@ -554,6 +770,20 @@ size_t k9_workspace_bytes(const Launch& a) {
     return grid_waves(a, Tq) * ws_wave_bytes(Tq);
 }
 
+// One streaming call (see launch_k7_stream): every wave (two streams) continues its trellis
+// over [s.t_begin, s.t_end) and emits the final bits (stream_traceback9).
+hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s) {
+    if (a.frames == 0) return hipSuccess;
+    if (!a.ws || !s.state || !s.out_bits || s.ring < 48 || s.ring % 48 || s.t_begin % 48 || s.t_end % 48)
+        return hipErrorInvalidValue;
+    auto kern = a.soft ? k9_kernel<true, false, true> : k9_kernel<false, false, true>;
+    const size_t waves = (a.frames + 1) / 2;
+    hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), (size_t)kRingBytes, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, 0, a.T, s.t_end, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws),
+                       size_t(kColBytes) / 16 * size_t(s.ring), s);
+    return hipGetLastError();
+}
+
 hipError_t launch_k9(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (!a.ws) return hipErrorInvalidValue;
@@ -569,7 +799,7 @@ hipError_t launch_k9(const Launch& a) {
     }
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
-                       static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq));
+                       static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq), StreamArgs());
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipSuccess;

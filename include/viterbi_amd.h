@@ -180,7 +180,7 @@ int vtb_device_count(void);
  * TODO (block traceback with early output, :195,199; src/viterbiDecoder.h:22-25):
  *   - each call pushes `segments` more coded segments per stream (row i of d_in, same layout
  *     as a frame's input: 1 byte per segment hard, 2 bytes soft), any count >= 0;
- *   - bits are emitted as soon as they are final: once the survivor paths of all 64 states
+ *   - bits are emitted as soon as they are final: once the survivor paths of all states
  *     have merged behind them no later input can change them, so the concatenation of a
  *     frame's outputs equals the whole-frame decode (vtb_decode_*, the reference's output)
  *     bit for bit;
@@ -188,11 +188,13 @@ int vtb_device_count(void);
  *     return of (segments - K)/8 + 1 bytes, last byte zero-padded), and every stream starts
  *     a new frame with the next call.  A frame has at least K segments in total.
  * Frames are not limited to VTB_MAX_FRAME_BITS: survivors live in a per-stream ring of
- * `window_steps` trellis steps (rounded up to a multiple of 48; <= 0 selects 49152) in
+ * `window_steps` trellis steps (rounded up to a multiple of 48; <= 0: the default below) in
  * device memory.  Output bits wait until the paths merge; should a stream go window_steps
  * steps without a merge (pure-noise input), its frame is lost: d_out_bits reports -1 for it
  * until the call with last != 0, after which it restarts cleanly.
- * K = 7 only (VTB_ERR_UNSUPPORTED otherwise); hard or soft input as for plans. */
+ * K = 7 and K = 9 (VTB_ERR_UNSUPPORTED otherwise); hard or soft input as for plans.  The ring
+ * holds 16 (K = 7) or 64 (K = 9) bytes per step per pair of streams; window_steps <= 0 selects
+ * 49152 steps at K = 7 and 12288 at K = 9. */
 typedef struct vtb_stream vtb_stream_t;
 
 int vtb_stream_create(vtb_stream_t** s, const vtb_code_t* code, vtb_input_t input, size_t streams,

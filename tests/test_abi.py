@@ -99,7 +99,9 @@ def test_plan_without_gpu_fails_loudly():
     stream = ctypes.c_void_p()
     assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(c), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
     k9 = native.VtbCode.make(9, CODES[9])
-    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k9), 0, 8, 0, 0) == native.VTB_ERR_UNSUPPORTED
+    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k9), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
+    k5 = native.VtbCode.make(5, CODES[5])
+    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k5), 0, 8, 0, 0) == native.VTB_ERR_UNSUPPORTED
 
 
 @pytest.mark.parametrize("F", [0, 1, 2, 3, 7, 100, 1001, 4096, 131072, 2**20, 2**20 + 5, 2**40 + 3])

@@ -224,14 +224,20 @@ def test_full_size_soft_batch_properties(orc):
     assert (o1[sub] == orc.decode(K, CODES[K], noisy[sub], L, soft=True)).all()
 
 
-def test_k9_full_config(orc, kernel):
-    """C4: K=9 hard, 4096 x 1024 -- oracle on a strided subset, round trip on all."""
+@pytest.mark.parametrize("soft", [False, True])
+def test_k9_full_config(orc, kernel, soft):
+    """C4: K=9, 4096 x 1024 -- every frame against the oracle (hard at BSC p = 0.03, soft at
+    the bench's SNR), and the decoded BER."""
     K, L, F = 9, 1024, 4096
     kernel.need(K)
-    unc, rx = random_frames(orc, K, L, F, 0.03, 99)
-    got = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L).decode_host(rx)
-    sub = np.arange(0, F, 37)
-    assert (got[sub] == orc.decode(K, CODES[K], rx[sub], L)).all()
+    if soft:
+        unc, rx = random_frames(orc, K, L, F, 0.0, 99, soft=True, sigma=0.63)
+    else:
+        unc, rx = random_frames(orc, K, L, F, 0.03, 99)
+    got = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft).decode_host(rx)
+    ref = orc.decode(K, CODES[K], rx, L, soft=soft, threads=16)
+    mism = np.flatnonzero((got != ref).any(axis=1))
+    assert mism.size == 0, f"{mism.size} of {F} frames differ (first {mism[:8]})"
     ber = np.unpackbits(got ^ unc).mean()
     assert ber < 1e-3
 

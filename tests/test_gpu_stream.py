@@ -182,8 +182,8 @@ def test_stream_api_errors():
     L = native.lib()
     c = CODE._c()
     h = ctypes.c_void_p()
-    k9 = ConvCode(9, CODES[9])._c()
-    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(k9), 0, 4, 0, 0) == native.VTB_ERR_UNSUPPORTED
+    k5 = ConvCode(5, CODES[5])._c()
+    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(k5), 0, 4, 0, 0) == native.VTB_ERR_UNSUPPORTED
     assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(c), 0, 0, 0, 0) == native.VTB_ERR_INVALID
     vs = ViterbiStream(CODE, streams=2, window_steps=96)
     x = torch.zeros((2, 100), dtype=torch.uint8, device="cuda")
