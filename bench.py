@@ -359,8 +359,11 @@ def main():
             ev1.record(stream)
 
         state["i"] = 0
+        # ev0 is enqueued before the timed region opens (the stream is idle after the warm-up
+        # synchronisation, so it completes at once; kernel_ms still spans t0 -> first kernel)
+        ev0.record(stream)
         t_issue0 = time.perf_counter()
-        elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=issued)
+        elapsed = timer.run(step, args.steps, on_end=issued)
         issue["us"] = (issue["s"] - t_issue0) / args.steps * 1e6
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 

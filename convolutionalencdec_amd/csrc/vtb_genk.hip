@@ -54,6 +54,85 @@ GenLayout gen_layout(int N, int E, int T, int L, int R, int k, bool gdec) {
     return l;
 }
 
+// N <= 64 states: one state per lane, its metric in a register, the 2^k predecessors gathered
+// with ds_bpermute, the lane's 2^k edge labels (time-invariant) in registers; k is a template
+// parameter so every per-edge loop is unrolled.
+template <int KB>
+__device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
+                                       int32_t* met, uint64_t* dec, int lane) {
+    constexpr int E = 1 << KB;
+    const int d = lane;
+    const bool live = d < N;
+    int32_t m = live ? met[d] : 0;
+    uint32_t lab[E];
+    int srcl[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int src = live ? (d >> KB) | (e << (kS - KB)) : 0;
+        srcl[e] = src << 2;
+        lab[e] = live ? uint32_t(tab[(src << KB) | (d & (E - 1))]) : 0u;
+    }
+    for (int t = 0; t < T; t++) {
+        const uint32_t rx = inb[t] & nmask;
+        uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const uint32_t pm = uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], m)) + uint32_t(__popc(lab[e] ^ rx));
+            best = min(best, (pm << 4) | uint32_t(e));
+        }
+        m = int32_t(best >> 4);
+        const int be = int(best & 15u);
+#pragma unroll
+        for (int j = 0; j < KB; j++) {
+            const uint64_t w = __ballot(live && ((be >> j) & 1));
+            if (lane == j) dec[size_t(t) * KB + j] = w;
+        }
+    }
+}
+
+// N = 256 states (k * S = 8: k = 1, 2 or 4), four states per lane: d = 64 r + lane.  The
+// 4 * 2^k edge labels of a lane's states are time-invariant and sit in registers (compile-time
+// indices: k is a template parameter), the previous metrics in LDS (double-buffered).
+template <int KB>
+__device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
+                                       int32_t* met, uint64_t* dec, int lane) {
+    constexpr int E = 1 << KB, kS = 8, N = 256;
+    uint32_t lab[4][E];
+    int sbase[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int d = r * 64 + lane;
+        sbase[r] = d >> KB;
+#pragma unroll
+        for (int e = 0; e < E; e++) lab[r][e] = uint32_t(tab[(((d >> KB) | (e << (kS - KB))) << KB) | (d & (E - 1))]);
+    }
+    int cur = 0;
+    for (int t = 0; t < T; t++) {
+        const uint32_t rx = inb[t] & nmask;
+        const int32_t* mc = met + cur * N;
+        int32_t* mn = met + (cur ^ 1) * N;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const uint32_t pm = uint32_t(mc[sbase[r] | (e << (kS - KB))]) + uint32_t(__popc(lab[r][e] ^ rx));
+                best = min(best, (pm << 4) | uint32_t(e));
+            }
+            mn[r * 64 + lane] = int32_t(best >> 4);
+            const int be = int(best & 15u);
+#pragma unroll
+            for (int j = 0; j < KB; j++) {
+                const uint64_t w = __ballot((be >> j) & 1);
+                if (lane == j) dec[(size_t(t) * 4 + r) * KB + j] = w;
+            }
+        }
+        cur ^= 1;
+        __syncthreads();
+    }
+    (void)a;
+}
+
 // GDEC: decision words in a global workspace (one slot per frame of the launch) instead of
 // LDS, for trellises whose words would hold the CU to one or two waves.
 template <bool GDEC>
@@ -85,65 +164,22 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
     __syncthreads();
 
+    // Candidates carry their predecessor index: cand = (pm << 4) | e, so one min gives the
+    // metric and the first minimum (lowest e among equal metrics, the reference's argmin).
     if (R == 1) {
-        // N <= 64: one state per lane, metrics in a register, predecessors gathered with
-        // ds_bpermute, the lane's 2^k edge labels (time-invariant) in registers
-        const int d = lane;
-        const bool live = d < N;
-        int32_t m = live ? met[d] : 0;
-        uint32_t lab[16];
-        int srcl[16];
-#pragma unroll
-        for (int e = 0; e < 16; e++) {
-            const int src = live ? (d >> k) | (e << (kS - k)) : 0;
-            srcl[e] = src << 2;
-            lab[e] = (e < E && live) ? uint32_t(tab[(src << k) | (d & (E - 1))]) : 0u;
-        }
-        for (int t = 0; t < T; t++) {
-            const uint32_t rx = inb[t];
-            int32_t best = 0;
-            int be = 0;
-#pragma unroll
-            for (int e = 0; e < 16; e++) {
-                if (e < E) {
-                    const int32_t pm = __builtin_amdgcn_ds_bpermute(srcl[e], m) + int32_t(__popc((lab[e] ^ rx) & nmask));
-                    if (e == 0 || pm < best) best = pm, be = e;  // first minimum
-                }
-            }
-            m = best;
-            for (int j = 0; j < k; j++) {
-                const uint64_t w = __ballot(live && ((be >> j) & 1));
-                if (lane == j) dec[size_t(t) * k + j] = w;
-            }
+        switch (k) {
+            case 1: acs_r1<1>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
+            case 2: acs_r1<2>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
+            case 3: acs_r1<3>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
+            default: acs_r1<4>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
         }
         __syncthreads();
+    } else if (k == 1) {
+        acs_r4<1>(a, T, inb, nmask, tab, met, dec, lane);
+    } else if (k == 2) {
+        acs_r4<2>(a, T, inb, nmask, tab, met, dec, lane);
     } else {
-        int cur = 0;
-        for (int t = 0; t < T; t++) {
-            const uint32_t rx = inb[t];
-            const int32_t* mc = met + cur * N;
-            int32_t* mn = met + (cur ^ 1) * N;
-            for (int r = 0; r < R; r++) {
-                const int d = r * 64 + lane;
-                int be = 0;
-                if (d < N) {
-                    const int bits = d & (E - 1);
-                    int32_t best = 0;
-                    for (int e = 0; e < E; e++) {
-                        const int src = (d >> k) | (e << (kS - k));
-                        const int32_t pm = mc[src] + int32_t(__popc((uint32_t(tab[(src << k) | bits]) ^ rx) & nmask));
-                        if (e == 0 || pm < best) best = pm, be = e;  // first minimum
-                    }
-                    mn[d] = best;
-                }
-                for (int j = 0; j < k; j++) {
-                    const uint64_t w = __ballot((be >> j) & 1);
-                    if (lane == j) dec[(size_t(t) * R + r) * k + j] = w;
-                }
-            }
-            cur ^= 1;
-            __syncthreads();
-        }
+        acs_r4<4>(a, T, inb, nmask, tab, met, dec, lane);
     }
 
     if (lane == 0) {  // traceback from state 0 (terminated frame)

@@ -30,6 +30,10 @@ struct Launch {
     // traceback and at exit, shader-clock at entry and exit, HW_ID and XCC_ID.  Null in
     // production (one uniform branch per stamp).
     unsigned long long* tstamp = nullptr;
+    // K=7 global-survivor variant: steps [0, gs_steps) keep their survivor words in the global
+    // workspace, the newest steps [gs_steps, Tpad) in LDS (set by the launcher; all global when
+    // >= Tpad)
+    int gs_steps = 1 << 30;
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
@@ -40,7 +44,8 @@ void set_debug_tstamp(unsigned long long* p);
 // Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
 // kernel: bit 2 skip traceback verification, bit 3 warm-up walk only, bit 4 return at entry, bit 5
 // one wave per frame pair instead of the persistent grid, bit 6 streaming survivors in the
-// global ring only, bit 8 never split frames across the halves of a wave).  Never
+// global ring only, bit 8 never split frames across the halves of a wave, bit 10 no
+// single-frame SEG kernel, bit 11 global-survivor variant without the LDS part).  Never
 // set in production; outputs are garbage when set.
 inline int debug_flags() {
     const char* v = getenv("VTB_DEBUG");

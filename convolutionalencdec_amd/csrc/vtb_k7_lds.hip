@@ -72,6 +72,7 @@
 // the time depends on how fast survivor paths merge.
 
 #include <type_traits>
+#include <utility>
 
 #include "vtb_k7_common.h"
 
@@ -301,6 +302,65 @@ __device__ __forceinline__ uint64_t tb_body8(uint32_t cb, uint32_t& l4, uint64_t
         bits |= uint64_t((u & 0x3Cu) | ((v >> 6) & 3u) | ((u & 3u) << 6)) << (8 * k);
         a = (a & ~0xFCu) | (rotl6c(v & 63u, r0) << 2);
     }
+    l4 = a & 0xFCu;
+    return bits;
+}
+
+// The same two walks for the global-survivor variant with its newest steps' words in LDS:
+// a lane's block is in LDS (is_lds: word at LDS byte lds_off + a) or in the workspace (gbase
+// + a).  Every window issues both an LDS read and a global load -- the one the lane does not
+// need at a harmless address (low LDS bytes / the slot's first, cache-hot column) -- and waits
+// for both once, so LDS lanes and global lanes of a wave walk at the same time (a per-lane
+// branch would run the two kinds one after the other; flat loads measured 40 % slower).
+template <int O>
+__device__ __forceinline__ uint32_t dual_ld16(uint32_t a, bool is_lds, uint32_t lds_off, uint64_t gbase) {
+    const uint32_t al = is_lds ? lds_off + a : (a & 0xFFu), ag = is_lds ? (a & 0xFFu) : a;
+    uint32_t vl, vg;
+    asm volatile("ds_read_u16 %0, %2 offset:%4\n\tglobal_load_ushort %1, %3, %5 offset:%4\n\ts_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : "=&v"(vl), "=&v"(vg) : "v"(al), "v"(ag), "i"(O), "s"(gbase));
+    return is_lds ? vl : vg;
+}
+template <int O>
+__device__ __forceinline__ uint32_t dual_ld8(uint32_t a, bool is_lds, uint32_t lds_off, uint64_t gbase) {
+    const uint32_t al = is_lds ? lds_off + a : (a & 0xFFu), ag = is_lds ? (a & 0xFFu) : a;
+    uint32_t vl, vg;
+    asm volatile("ds_read_u8 %0, %2 offset:%4\n\tglobal_load_ubyte %1, %3, %5 offset:%4\n\ts_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : "=&v"(vl), "=&v"(vg) : "v"(al), "v"(ag), "i"(O), "s"(gbase));
+    return is_lds ? vl : vg;
+}
+template <int... Is, class F>
+__device__ __forceinline__ void static_for_k7(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+__device__ __forceinline__ uint64_t tb_body_dual(uint32_t cb, uint32_t& l4, bool is_lds, uint32_t lds_off,
+                                                 uint64_t gbase) {
+    uint32_t a = cb | l4;
+    uint64_t bits = 0;
+    static_for_k7(std::make_integer_sequence<int, 24>{}, [&](auto jc) {
+        constexpr int j = decltype(jc)::value, todd = 47 - 2 * j;
+        if (j % 3 == 0) bits |= uint64_t((a >> 2) & 63u) << (6 * (7 - j / 3));
+        constexpr int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+        const uint32_t v = dual_ld16<(todd >> 4) * 256>(a, is_lds, lds_off, gbase);
+        constexpr int pos = 2 + (todd - 1) % 6;
+        uint32_t fld;
+        if constexpr (pos >= sh) fld = v << (pos - sh);
+        else fld = v >> (sh - pos);
+        a = (a & ~(3u << pos)) | (fld & (3u << pos));
+    });
+    l4 = a & 0xFCu;
+    return bits;
+}
+__device__ __forceinline__ uint64_t tb_body8_dual(uint32_t cb, uint32_t& l4, bool is_lds, uint32_t lds_off,
+                                                  uint64_t gbase) {
+    uint32_t a = cb | l4;
+    uint64_t bits = 0;
+    static_for_k7(std::make_integer_sequence<int, 6>{}, [&](auto kc) {
+        constexpr int k = 5 - decltype(kc)::value, r0 = (8 * k) % 6;
+        const uint32_t u = rotr6c((a >> 2) & 63u, r0);
+        const uint32_t v = dual_ld8<256 * (k >> 1) + (k & 1)>(a, is_lds, lds_off, gbase);
+        bits |= uint64_t((u & 0x3Cu) | ((v >> 6) & 3u) | ((u & 3u) << 6)) << (8 * k);
+        a = (a & ~0xFCu) | (rotl6c(v & 63u, r0) << 2);
+    });
     l4 = a & 0xFCu;
     return bits;
 }
@@ -817,6 +877,10 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t msave = 0;                                      // (SPLIT) frame B's metrics at t1
     // first step of this launch: 0, or (streaming) where the previous call stopped
     const int tbeg = STREAM ? sa.t_begin : 0;
+    // GS (frames): survivor words of steps [0, tg) in the global workspace, of [tg, Tpad) in
+    // LDS at r0 (the newest steps: the traceback's first walks read LDS)
+    const int tg = GS && !STREAM ? table.gs_steps : (1 << 30);
+    const int lds_t0 = (STREAM && !GS) ? tbeg : GS ? tg : 0;  // step of the first LDS word column
     if constexpr (STREAM) {
         if (tbeg > 0) M = sa.state[wp * kStreamStateWords + lane];
     }
@@ -843,12 +907,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const int tacs = (dbg & 2) ? 0 : (SPLIT && sp ? t1s : Tpad);
     // One 48-step chunk of the ACS (fully unrolled); PADTAG: this chunk stages the chunk that
     // holds step T (padding rows possible).
-    auto acs_chunk = [&](const int t0, auto padtag) __attribute__((always_inline)) {
+    // gtag: this chunk's survivor words go to the global workspace (else LDS)
+    auto acs_chunk = [&](const int t0, auto padtag, auto gtag) __attribute__((always_inline)) {
+        constexpr bool GSC = decltype(gtag)::value;
         const int c0 = t0 / kChunk;
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
-        uint32_t* dchunk = dec + (((STREAM && !GS) ? t0 - tbeg : t0) >> 4) * 64 + widx;  // (stream: this call's words)
+        uint32_t* dchunk = dec + ((t0 - lds_t0) >> 4) * 64 + widx;  // (LDS words; stream: this call's)
         // GS: byte offset of the lane's words (streaming: position in the survivor ring)
         const uint32_t gvo = 4u * (((STREAM ? t0 % sa.ring : t0) >> 4) * 64 + widx);
 
@@ -874,7 +940,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
                 z = bfi_op(0x0F0F0F0Fu, z, pw[2] << 4);                                          \
                 z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
-                VTB_EXP_WORD(store_word<GS>(dchunk, gvo, gbase, ((I) >> 4), z));                  \
+                VTB_EXP_WORD(store_word<GSC>(dchunk, gvo, gbase, ((I) >> 4), z));                 \
             }                                                                                    \
         }                                                                                        \
         if (!SOFT && ((I) & 7) == 7) {                                                           \
@@ -883,7 +949,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 m_prev = M;                                                                      \
             } else {                                                                             \
                 const uint32_t z = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
-                VTB_EXP_WORD(store_word<GS>(dchunk, gvo, gbase, ((I) >> 4), z));                  \
+                VTB_EXP_WORD(store_word<GSC>(dchunk, gvo, gbase, ((I) >> 4), z));                 \
             }                                                                                    \
             M = VTB_RENORM_APPLY(I) ? ((M & ~H::MASK) + dd) : (M & ~H::MASK);                    \
         }                                                                                        \
@@ -891,7 +957,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #define VTB_GROUP(G)                                                                              \
     {                                                                                             \
         if ((G) == 0) load_raw(c0 + 1, ra, rb);                                                   \
-        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set, false);                            \
+        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set, !GSC);                             \
         if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
             stage_write(c0 + 1, se, set, padtag);                                                 \
         }                                                                                         \
@@ -939,10 +1005,19 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         if (second && (t0 - tbeg) / kChunk < hi_chunks) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
     };
+    // one chunk, its survivor words to the global workspace (GS, steps before tg) or to LDS
+    auto run_chunk = [&](const int t0, auto padtag) __attribute__((always_inline)) {
+        if constexpr (GS) {
+            if (t0 < tg) acs_chunk(t0, padtag, std::true_type{});
+            else acs_chunk(t0, padtag, std::false_type{});
+        } else {
+            acs_chunk(t0, padtag, std::false_type{});
+        }
+    };
     if constexpr (SPLIT) {
         for (int t0 = 0; t0 < tacs; t0 += kChunk) {
             prio(t0);
-            acs_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
+            run_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
             if (t0 == warm - kChunk) msave = M;
         }
     } else {
@@ -951,14 +1026,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         int t0 = tbeg;
         for (; t0 < tstage; t0 += kChunk) {
             prio(t0);
-            acs_chunk(t0, std::false_type{});
+            run_chunk(t0, std::false_type{});
         }
         if (t0 == tstage) {
             prio(t0);
-            acs_chunk(t0, std::true_type{});
+            run_chunk(t0, std::true_type{});
             t0 += kChunk;
         }
-        if (t0 < tacs) acs_chunk(t0, std::false_type{});
+        if (t0 < tacs) run_chunk(t0, std::false_type{});
     }
     __builtin_amdgcn_s_setprio(0);
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written
@@ -1000,16 +1075,27 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const bool known = (SPLIT && sp) ? (f == 1 && start >= Tb) || (f == 0 && blk >= nA) || (f == 1 && lane < kB0)
                                      : start >= T;
     const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbp) / 48;  // dbg bit 3: warm-up walk only
+    // GS with LDS words for the newest steps: per block (lane) LDS or global, both walked at once
+    const bool hyb = GS && tg < Tpad;
+    const uint32_t lds_off = uint32_t(r0) - 16u * uint32_t(GS ? tg : 0);  // LDS byte of word offset a
     auto tb48 = [&](uint32_t cb, uint32_t& l4) {
         if constexpr (SOFT) return tb_body<GS>(cb, l4, gbase);
         else return tb_body8<GS>(cb, l4, gbase);
+    };
+    auto tb48t = [&](int tlo, uint32_t& l4) -> uint64_t {  // the 48 steps at tlo
+        const uint32_t cb = cb0 + 256 * (tlo >> 4);
+        if (GS && hyb) {
+            if constexpr (SOFT) return tb_body_dual(cb, l4, tlo >= tg, lds_off, gbase);
+            else return tb_body8_dual(cb, l4, tlo >= tg, lds_off, gbase);
+        }
+        return tb48(cb, l4);
     };
     uint32_t loc = 0, loc_top = 0;  // survivor location as 4 l'
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
         if (tlo < start) {  // lane's walk has begun (start is a multiple of 48)
-            const uint64_t bits = tb48(cb0 + 256 * (tlo >> 4), loc);
+            const uint64_t bits = tb48t(tlo, loc);
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
@@ -1039,7 +1125,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
                 const int tlo = start_full - 48 * (g + 1);
-                put_bits48(ob, tlo, tb48(cb0 + 256 * (tlo >> 4), loc));
+                put_bits48(ob, tlo, tb48t(tlo, loc));
             }
             fin = loc;
             fixed = true;
@@ -1145,17 +1231,18 @@ __global__ __launch_bounds__(256) void k7_seg_kernel(const uint8_t* __restrict__
     {
         const uint8_t* src = in + size_t(blockIdx.x) * in_stride;
         const int nin = (SOFT ? 2 : 1) * T;
-        uint4 v[kSegLoads];
-#pragma unroll
-        for (int j = 0; j < kSegLoads; j++) {
-            const int i = 16 * int(threadIdx.x + j * blockDim.x);
-            if (i < nin) v[j] = *reinterpret_cast<const uint4*>(src + i);
-        }
-#pragma unroll
-        for (int j = 0; j < kSegLoads; j++) {
-            const int i = 16 * int(threadIdx.x + j * blockDim.x);
-            if (i < nin) *reinterpret_cast<uint4*>(smem + sg.in_lds + i) = v[j];
-        }
+        const int step = 16 * int(blockDim.x), i0 = 16 * int(threadIdx.x);
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
+        static_assert(kSegLoads == 4, "four staging loads per thread");
+        if (i0 < nin) v0 = *reinterpret_cast<const uint4*>(src + i0);
+        if (i0 + step < nin) v1 = *reinterpret_cast<const uint4*>(src + i0 + step);
+        if (i0 + 2 * step < nin) v2 = *reinterpret_cast<const uint4*>(src + i0 + 2 * step);
+        if (i0 + 3 * step < nin) v3 = *reinterpret_cast<const uint4*>(src + i0 + 3 * step);
+        uint8_t* dst = smem + sg.in_lds + i0;
+        if (i0 < nin) *reinterpret_cast<uint4*>(dst) = v0;
+        if (i0 + step < nin) *reinterpret_cast<uint4*>(dst + step) = v1;
+        if (i0 + 2 * step < nin) *reinterpret_cast<uint4*>(dst + 2 * step) = v2;
+        if (i0 + 3 * step < nin) *reinterpret_cast<uint4*>(dst + 3 * step) = v3;
     }
     __syncthreads();
     uint32_t off[6];
@@ -1254,13 +1341,27 @@ __global__ __launch_bounds__(256) void k7_seg_kernel(const uint8_t* __restrict__
     }
 }
 
-// LDS of the survivor-in-global variant: table ring and decoded bytes only.
-size_t lds_bytes_gs(int T) { return (size_t)region0(T); }
+// Newest steps whose survivor words the global-survivor variant keeps in LDS: as many 48-step
+// chunks as leave 8 waves per CU (2 per SIMD, where the ACS saturates the VALU) their LDS;
+// HBM then sees only the older steps' words.  Hard input only: its traceback reads one byte
+// per 8 steps, and config C3 hard ran 1-2 % faster (0.835 vs 0.843-0.851 ms, 65,536 x 2,048
+// bits); soft input reads a word per 2 steps, and a wave walks at the pace of its slowest
+// lane, so the LDS lanes gained nothing while every window paid for both loads: C3 soft
+// 1.16-1.17 vs 1.07 ms (profiles/r02/hybrid_survivors_ab.txt).  VTB_DEBUG bit 11
+// (measurement only): none.
+int gs_lds_steps(int T, bool soft) {
+    if (soft || (debug_flags() & 2048)) return 0;
+    const int per_wave = 160 * 1024 / 8 - region0(T);
+    int s = per_wave > 0 ? per_wave / 16 / kChunk * kChunk : 0;
+    return s < t_pad(T) ? s : t_pad(T);
+}
+// LDS of the survivor-in-global variant: table ring, decoded bytes and the newest steps' words.
+size_t lds_bytes_gs(int T, bool soft) { return (size_t)region0(T) + 16 * (size_t)gs_lds_steps(T, soft); }
 size_t ws_wave_bytes(int T) { return 16 * (size_t)t_pad(T); }
 constexpr size_t kMaxWsBytes = size_t(1) << 30;  // survivor workspace cap (global variant)
 
 template <bool GS>
-size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T) : lds_bytes(a.T); }
+size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T, a.soft) : lds_bytes(a.T); }
 
 template <bool GS, bool LOOP = true, bool SPLIT = false>
 auto kernel_of(const Launch& a) {
@@ -1315,8 +1416,10 @@ hipError_t launch_k7(const Launch& a) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
+    Launch la = a;
+    la.gs_steps = GS ? t_pad(a.T) - gs_lds_steps(a.T, a.soft) : (1 << 30);
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), a,
+                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), la,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
     return hipGetLastError();
 }
@@ -1329,7 +1432,7 @@ size_t k7_lds_bytes(const Launch& a) { return lds_bytes(a.T); }
 
 hipError_t launch_k7_lds(const Launch& a) { return launch_k7<false>(a); }
 
-bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T) <= 160 * 1024; }
+bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T, a.soft) <= 160 * 1024; }
 
 size_t k7_global_workspace_bytes(const Launch& a) { return grid_waves<true>(a) * ws_wave_bytes(a.T); }
 
