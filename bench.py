@@ -109,6 +109,16 @@ def cpu_model():
     return None
 
 
+def cgroup_cpus():
+    """CPUs' worth of time this process may use (cgroup v2 cpu.max quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds, threads, frame_bits):
     """Reference decoder (oracle/_ref/libref_k7.so, compiled from the reference sources) on
     this host: the speedDecode protocol (speedDecode.c:37-116) with the workload's frame
@@ -139,7 +149,7 @@ def cpu_baseline(seconds, threads, frame_bits):
             os.close(saved)
         return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
                 "single_core_value": round(one, 2), "single_core_value_2048bit": round(one_2048, 2),
-                "cpu_model": cpu_model(), "host_cpus_available": avail,
+                "cpu_model": cpu_model(), "host_cpus_available": avail, "cgroup_cpu_quota": cgroup_cpus(),
                 "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
                           f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "
                           f"{seconds:g} s, one decoder state per thread"}
