@@ -182,24 +182,65 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         acs_r4<4>(a, T, inb, nmask, tab, met, dec, lane);
     }
 
-    if (lane == 0) {  // traceback from state 0 (terminated frame)
-        int s = 0;
-        for (int t = T - 1; t >= 0; t--) {
-            if (t < T - a.S) {
-                const int seg = s & (E - 1);
-                for (int j = 0; j < k; j++) {
-                    const int pos = t * k + j;
-                    if ((seg >> (k - 1 - j)) & 1) outb[pos >> 3] |= uint8_t(0x80u >> (pos & 7));
-                }
-            }
+    // Traceback from state 0 (terminated frame), block-parallel and verified (the K=7
+    // kernel's scheme, vtb_k7_lds.hip): lane b walks steps [b tbb, (b+1) tbb) back from
+    // kGenWarm steps past its block's end, starting from state 0 there (exact when the walk
+    // starts at T).  A block is right if it entered on its successor's exit state and that
+    // successor is proven; failed blocks re-walk from a proven successor until all are
+    // proven.  Then every lane emits its block's bits (LDS atomic OR: blocks share bytes).
+    {
+        constexpr int kGenWarm = 96;
+        auto pred = [&](int s, int t) {
             const uint64_t* w = dec + (size_t(t) * R + (s >> 6)) * k;
             int e = 0;
             for (int j = 0; j < k; j++) e |= int((w[j] >> (s & 63)) & 1u) << j;
-            s = (s >> k) | (e << (kS - k));
+            return (s >> k) | (e << (kS - k));
+        };
+        const int tbb = (T + 63) / 64, lo = lane * tbb, top = min(lo + tbb, T);
+        const bool active = lo < T;
+        const int start = min(top + kGenWarm, T);
+        int s = 0;
+        for (int t = start - 1; active && t >= top; t--) s = pred(s, t);
+        int s_top = s;
+        for (int t = top - 1; active && t >= lo; t--) s = pred(s, t);
+        int fin = s;
+        bool fixed = !active || start == T;
+        for (int round = 0; round < 65; round++) {
+            const int sf = __shfl_down(fin, 1);
+            const bool ok = fixed || s_top == sf;
+            const uint64_t bad = ~__ballot(ok);
+            if (bad == 0) break;
+            if (!ok && (bad >> (lane + 1)) == 0) {
+                s_top = s = sf;
+                for (int t = top - 1; t >= lo; t--) s = pred(s, t);
+                fin = s;
+                fixed = true;
+            }
         }
+        uint32_t* ow = reinterpret_cast<uint32_t*>(outb);
+        uint32_t acc = 0;
+        int wcur = -1;
+        s = s_top;
+        for (int t = top - 1; active && t >= lo; t--) {
+            if (t < T - a.S) {
+                const int seg = s & (E - 1);
+                for (int j = 0; j < k; j++) {
+                    if ((seg >> (k - 1 - j)) & 1) {
+                        const int pos = t * k + j;
+                        if ((pos >> 5) != wcur) {
+                            if (acc) atomicOr(ow + wcur, acc);
+                            wcur = pos >> 5, acc = 0;
+                        }
+                        acc |= 1u << (8 * ((pos >> 3) & 3) + 7 - (pos & 7));
+                    }
+                }
+            }
+            s = pred(s, t);
+        }
+        if (acc) atomicOr(ow + wcur, acc);
     }
     __syncthreads();
-    uint8_t* orow = out + f * out_stride;  // (GDEC: lane 0 read its own stores back)
+    uint8_t* orow = out + f * out_stride;  // (GDEC: each lane read the decision words its walks need)
     for (int i = lane; i < a.L / 8; i += 64) orow[i] = outb[i];
 }
 

@@ -78,3 +78,45 @@ def test_random_case_vs_oracle(orc, case):
         got = d.decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
     bad = np.flatnonzero((got != want).any(axis=1))
     assert bad.size == 0, (case, bad.size, bad[:8])
+
+
+def _frame_cases(n=48, seed=20261017):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        soft = bool(rng.integers(0, 2))
+        L = int(rng.integers(1, 4090 if soft else 8100))
+        noise = float(rng.choice([0.0, 0.03, 0.07, 0.5]))
+        out.append((i, L, soft, noise))
+    return out
+
+
+@pytest.mark.parametrize("case", _frame_cases(), ids=lambda c: f"{c[0]}-L{c[1]}-{'soft' if c[2] else 'hard'}-p{c[3]}")
+def test_single_frame_path_vs_oracle(orc, case, monkeypatch):
+    """vtb_decode_frame_sync (the segmented single-frame kernel, or its frame-kernel fallback
+    when a segment has not converged) at random frame lengths and noise levels."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    i, L, soft, noise = case
+    if soft:
+        sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
+        unc, x = random_frames(orc, 7, L, 3, 0.0, 5000 + i, soft=True, sigma=sigma)
+    else:
+        unc, x = random_frames(orc, 7, L, 3, noise, 5000 + i)
+    x = np.ascontiguousarray(x).reshape(3, -1)
+    want = orc.decode(7, CODES[7], x, L, soft=soft, threads=THREADS)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L, soft=soft)
+    got = np.stack([d.decode_frame(r) for r in x])
+    assert (got == want).all(), case
+
+
+@pytest.mark.parametrize("L", [1100, 2047, 2048, 3001, 6000, 9999, 16384])
+@pytest.mark.parametrize("noise", [0.04, 0.5])
+def test_global_survivor_variant_hard_hybrid(orc, L, noise, monkeypatch):
+    """The K=7 global-survivor variant on hard input keeps its newest steps' words in LDS and
+    walks LDS and global blocks together; forced for every frame length."""
+    monkeypatch.setenv("VTB_KERNEL", "gws")
+    F = 129
+    unc, x = random_frames(orc, 7, L, F, noise, 7000 + L)
+    want = orc.decode(7, CODES[7], x, L, threads=THREADS)
+    got = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L).decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert (got == want).all()
