@@ -138,19 +138,51 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     __syncthreads();
     if (!valid) return;
 
-    // Terminated traceback from state 0 (reference :200-256).
-    auto decision = [&](int t, unsigned s) -> unsigned {
-        uint64_t w = dec[(size_t)t * R + (s / G)];
-        return unsigned(w >> (fi * G + (s % G))) & 1u;
+    // Terminated traceback from state 0 (reference :200-256), block-parallel and verified
+    // (the K=7 kernel's scheme, vtb_k7_lds.hip): the frame's G lanes each take a block of tbb
+    // steps (a multiple of 8: every block owns whole output bytes), walk back to it from
+    // kWarm steps past its end starting in state 0 there (exact when that is T, the
+    // terminated end), and a block is right once it entered on its successor's exit state and
+    // that successor is proven; failed blocks re-walk from a proven successor until all are.
+    // The state after step t is s; its bit 0 is the information bit of step t, and the
+    // predecessor is (s >> 1) | (decision << (S - 1)).
+    constexpr int kWarm = 8 * S + 48;
+    auto pred = [&](unsigned st, int t) -> unsigned {
+        const uint64_t w = dec[(size_t)t * R + (st / G)];
+        return (st >> 1) | (unsigned((w >> (fi * G + (st % G))) & 1u) << (S - 1));
     };
-    unsigned s = 0;
-    for (int i = 0; i < S; i++) s = (s >> 1) | (decision(T - 1 - i, s) << (S - 1));
+    const int tbb = ((T + G - 1) / G + 7) / 8 * 8;
+    const int lo = lam * tbb, top = lo + tbb < T ? lo + tbb : T;
+    const bool active = lo < T;
+    const int start = top + kWarm < T ? top + kWarm : T;
+    unsigned st = 0;
+    for (int t = start - 1; active && t >= top; t--) st = pred(st, t);
+    unsigned s_top = st;
+    for (int t = top - 1; active && t >= lo; t--) st = pred(st, t);
+    unsigned fin = st;
+    bool fixed = !active || start == T;
+    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << G) - 1)) << (fi * G);
+    for (int round = 0; round <= G; round++) {
+        const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
+        const bool ok = fixed || s_top == sf;
+        const uint64_t bad = ~__ballot(ok);
+        if (bad == 0) break;
+        const uint64_t badf = (bad & fmask) >> (fi * G);  // this frame's failed blocks
+        if (!ok && (badf >> (lam + 1)) == 0) {
+            st = s_top = sf;
+            for (int t = top - 1; t >= lo; t--) st = pred(st, t);
+            fin = st;
+            fixed = true;
+        }
+    }
+    if (!valid || !active) return;
     uint8_t* o = out + myframe * out_stride;
     unsigned byte = 0;
-    for (int t = L - 1; t >= 0; t--) {
-        byte = ((byte >> 1) | ((s & 1u) << 7)) & 0xffu;
-        if ((t & 7) == 0 && lam == 0) o[t >> 3] = uint8_t(byte);
-        s = (s >> 1) | (decision(t, s) << (S - 1));
+    st = s_top;
+    for (int t = top - 1; t >= lo; t--) {
+        byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
+        if ((t & 7) == 0 && t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
+        st = pred(st, t);
     }
 }
 
