@@ -37,7 +37,7 @@ def mean_counter(d, name):
 
 fetch_kib, nf = mean_counter("pmc_fetch", "FETCH_SIZE")
 write_kib, nw = mean_counter("pmc_write", "WRITE_SIZE")
-tag = key.split("_")[1]  # soft / hard: detail files per workload
+tag = key  # detail files per workload
 FETCH_CORRECTION = 2.0
 total = (FETCH_CORRECTION * fetch_kib + write_kib) * 1024.0
 os.makedirs(os.path.join(repo, "profiles", rnd), exist_ok=True)
