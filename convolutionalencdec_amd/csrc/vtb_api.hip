@@ -135,7 +135,8 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.tstamp = vtb::debug_tstamp();
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
     const char* force = std::getenv("VTB_KERNEL");
-    const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");  // (seg: vtb_decode_frame_sync)
+    const bool k7s = env_flag_is("VTB_KERNEL", "k7s");  // prefer the persistent split kernel (below)
+    const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg") || k7s;  // (seg: vtb_decode_frame_sync)
     const bool want_k7 = any || env_flag_is("VTB_KERNEL", "k7");
     const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
     const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
@@ -169,6 +170,20 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
         a.ws = p->ws;
         return true;
     };
+    // Longer K=7 soft frames (the LDS variant would hold the CU below 8 waves, e.g. config C3):
+    // one frame per wave as two halves with LDS survivors, persistent (launch_k7_split_loop),
+    // when the halves fit 8 waves per CU.  Measured on C3 shapes: soft 1.085
+    // vs 1.136 ms at SNR -5 dB (2.3 % of the frames re-decoded from the list), hard 0.887 vs
+    // 0.827 ms at p = 0.056 (9.6 % re-decoded; hard keeps the global variant).  VTB_KERNEL=k7s
+    // prefers it wherever it applies, hard input included; VTB_DEBUG bit 12 (measurement
+    // only): never.
+    const bool want_split = k7s || (any && !k7_in_lds && a.soft);
+    if (want_split && !(vtb::debug_flags() & 4096) && vtb::k7_split_loop_supported(a)) {
+        if (!workspace(vtb::k7_split_loop_workspace_bytes(a))) return VTB_ERR_NOMEM;
+        e = vtb::launch_k7_split_loop(a);
+        if (e == hipErrorOutOfMemory) return VTB_ERR_NOMEM;
+        return e == hipSuccess ? VTB_OK : VTB_ERR_DEVICE;
+    }
     if (k7_in_lds) {
         e = vtb::launch_k7_lds(a);
     } else if (want_gws && vtb::k7_global_supported(a)) {
@@ -321,6 +336,16 @@ const char* vtb_version(void) { return VTB_VERSION_STRING; }
 // Measurement only (not in include/viterbi_amd.h): device buffer of 8 u64 per wave that the
 // next K=7 frame launches fill with phase timestamps (tools/tstamp.py); nullptr turns it off.
 void vtb_debug_set_tstamp(unsigned long long* d_buf) { vtb::set_debug_tstamp(d_buf); }
+
+// Measurement only (not in include/viterbi_amd.h): frames of the plan's last persistent split
+// launch that did not converge split (re-decoded by the list kernel); synchronises the device.
+long long vtb_debug_split_failures(vtb_plan_t* plan) {
+    if (!plan || !plan->ws) return -1;
+    DeviceGuard g(plan->device);
+    uint32_t n = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&n, plan->ws, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
 
 // Testing only (not in include/viterbi_amd.h): how vtb_decode_frame_sync calls ended, SEG
 // kernel decoded / SEG not converged (re-decoded) / no SEG kernel for the plan.

@@ -34,6 +34,11 @@ struct Launch {
     // workspace, the newest steps [gs_steps, Tpad) in LDS (set by the launcher; all global when
     // >= Tpad)
     int gs_steps = 1 << 30;
+    // K=7 split frames (one frame per wave, two halves): warm-up steps of the second half (a
+    // multiple of 48), and for the persistent split kernel the list of frames whose halves did
+    // not converge ([0] = count, then frame indices; decoded again by the list kernel)
+    int split_warm = 96;
+    uint32_t* fail_list = nullptr;
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
@@ -72,6 +77,14 @@ hipError_t launch_k7_lds(const Launch& a);
 bool k7_global_supported(const Launch& a);
 size_t k7_global_workspace_bytes(const Launch& a);
 hipError_t launch_k7_global(const Launch& a);
+
+// K=7 persistent split kernel (vtb_k7_lds.hip): frames too long for the LDS variant at 8 waves
+// per CU decoded one per wave as two halves with LDS survivors, frames whose halves do not
+// converge re-decoded by the global-survivor kernel from a list; workspace = the list plus the
+// list kernel's survivor slots.
+bool k7_split_loop_supported(const Launch& a);
+size_t k7_split_loop_workspace_bytes(const Launch& a);
+hipError_t launch_k7_split_loop(const Launch& a);
 
 // K=7 single-frame latency path (k7_seg_kernel): one workgroup of up to 4 waves per frame,
 // the frame cut into up to 8 segments decoded at once (warm-up `warm` steps, a multiple of

@@ -115,7 +115,9 @@ int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
 // 2,000 simulated soft frames at SNR -5 dB (48: 98.2 %, and every miss costs its wave a
 // second, unsplit pass).
 constexpr int kSplitWarm = 96;
-__host__ __device__ constexpr int split_t1(int T) { return ((T + kSplitWarm) / 2 + kChunk - 1) / kChunk * kChunk; }
+__host__ __device__ constexpr int split_t1(int T, int warm = kSplitWarm) {
+    return ((T + warm) / 2 + kChunk - 1) / kChunk * kChunk;
+}
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
 int region0(int T) {  // multiple of 256: the traceback edits survivor-word addresses in place
@@ -661,6 +663,27 @@ __device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, s
     }
 }
 
+// The same for the persistent split kernel: chunk 0 of both halves of frame f (A from step 0,
+// B from step t1 - warm).
+template <bool SOFT>
+__device__ __forceinline__ void load_raw0_split(const uint8_t* in, size_t in_stride, int T, int t1, int warm, size_t f,
+                                                uint32_t& ra, uint32_t& rb) {
+    const int lane = threadIdx.x, srow = lane < kChunk ? lane : lane - kChunk;
+    constexpr uint32_t SB = SOFT ? 2 : 1;
+    const uint8_t* a = in + f * in_stride;
+    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(a));
+    const uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(a + SB * size_t(t1 - warm)));
+    const int Tb = T - t1 + warm;
+    const uint32_t tc = SB * uint32_t(srow < T ? srow : T - 1), tcb = SB * uint32_t(srow < Tb ? srow : Tb - 1);
+    if constexpr (SOFT) {
+        asm volatile("global_load_ushort %0, %2, %4\n\tglobal_load_ushort %1, %3, %5"
+                     : "=&v"(ra), "=&v"(rb) : "v"(tc), "v"(tcb), "s"(baseA), "s"(baseB));
+    } else {
+        asm volatile("global_load_ubyte %0, %2, %4\n\tglobal_load_ubyte %1, %3, %5"
+                     : "=&v"(ra), "=&v"(rb) : "v"(tc), "v"(tcb), "s"(baseA), "s"(baseB));
+    }
+}
+
 // SEG (the single-frame latency path, k7_seg_kernel): one frame over the waves of one
 // workgroup, 2 segments per wave in the u16 halves.  Segment i runs sg.n steps from
 // g_i = i (n - warm); its decisions are the frame's from s_i = g_i + warm on (s_0 = 0) once
@@ -680,7 +703,11 @@ struct SegArgs {
 // decodes after this one (its chunk 0 is prefetched into (pra, prb) before the traceback;
 // LDS variant only, whose traceback issues no global loads that would wait behind it).
 
-template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT, bool SEG = false>
+// LIST (global-survivor variant, persistent): pair wp is frames list[1 + 2wp], list[2 + 2wp] of
+// table.fail_list (the frames a persistent split launch could not decode split), `frames` = the
+// list's count.  SPLIT with LOOP (the persistent split kernel): a split pass that does not
+// converge appends the frame to table.fail_list instead of decoding it again in the wave.
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT, bool SEG = false, bool LIST = false>
 __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
@@ -688,6 +715,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                                         uint32_t& pra, uint32_t& prb, const uint32_t (&off)[6],
                                         const SegArgs* sgp = nullptr, uint32_t* seg_out = nullptr) {
     static_assert(!SEG || (SPLIT && !GS && !STREAM && !LOOP), "SEG runs the split pair on LDS survivors");
+    static_assert(!LIST || (GS && LOOP && !SPLIT && !STREAM), "the list kernel is the persistent global variant");
 
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
@@ -707,16 +735,20 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // SEG: wave wv runs segments 2wv (half A) and 2wv + 1 (half B; a copy of A if unused)
     const int segA = 2 * wv, segB = SEG && 2 * wv + 1 < sgp->G ? 2 * wv + 1 : 2 * wv;
     const int gA = SEG ? segA * (sgp->n - sgp->warm) : 0, gB = SEG ? segB * (sgp->n - sgp->warm) : 0;
-    const int warm = SEG ? sgp->warm : kSplitWarm;
-    const int t1s = SEG ? sgp->n : SPLIT ? split_t1(T) : 0;
+    const int warm = SEG ? sgp->warm : table.split_warm;
+    const int t1s = SEG ? sgp->n : SPLIT ? split_t1(T, warm) : 0;
     bool sp = SPLIT;                            // this pass runs split
-    int Tb = SEG ? T - gB : SPLIT ? T - t1s + kSplitWarm : T;  // frame B's steps (local)
-    const int Ta = SEG ? T - gA : T;                           // frame A's steps (local)
-    const size_t fa = SPLIT ? wp : wp * 2, fb = fa + 1;
-    const bool has_b = !SPLIT && fb < frames;
+    int Tb = SEG ? T - gB : SPLIT ? T - t1s + warm : T;  // frame B's steps (local)
+    const int Ta = SEG ? T - gA : T;                     // frame A's steps (local)
+    size_t fa = SPLIT ? wp : wp * 2, fb = fa + 1;
+    bool has_b = !SPLIT && fb < frames;
+    if constexpr (LIST) {
+        fa = table.fail_list[1 + 2 * wp];
+        fb = has_b ? table.fail_list[2 + 2 * wp] : fa;
+    }
     const uint64_t gbase = (GS || STREAM) ? uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave)) : 0;
     const uint8_t* inA = in + fa * in_stride;
-    const uint8_t* inB = SPLIT ? inA + (SOFT ? 2 : 1) * size_t(t1s - kSplitWarm)
+    const uint8_t* inB = SPLIT ? inA + (SOFT ? 2 : 1) * size_t(t1s - warm)
                                : in + (has_b ? fb : fa) * in_stride;  // lone last frame: B decodes a copy
 
     // Table staging: lane r < 48 builds the row of step 48c + r from the raw input bytes of
@@ -1048,14 +1080,30 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         stream_traceback<SOFT, GS>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, uint32_t(r0));
         return;
     }
-    if (LOOP && !GS && next < (frames + 1) / 2) load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
+    const size_t units = SPLIT ? frames : (frames + 1) / 2;  // (persistent loop: pairs, or split frames)
+    if (LOOP && !GS && next < units) {
+        if constexpr (SPLIT) load_raw0_split<SOFT>(in, in_stride, T, t1s, warm, next, pra, prb);
+        else load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
+    }
     if (SPLIT && sp) {
         // frame A's metrics at t1 against frame B's at its step 96 (= t1), histories masked:
         // equal up to a constant -> B's decisions from t1 on are the frame's
         constexpr uint32_t KEEP = 0xFFFFu & ~(H::SC - 1);
         const uint32_t a = M & KEEP, b = (msave >> 16) & KEEP;
         const uint32_t a0 = __builtin_amdgcn_readfirstlane(a), b0 = __builtin_amdgcn_readfirstlane(b);
-        if (__ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) != ~0ull) continue;
+        if (__ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) != ~0ull) {
+            if constexpr (LOOP) {
+                // persistent split kernel: the list kernel decodes this frame afterwards
+                if (lane == 0) {
+                    const uint32_t i = atomicAdd(table.fail_list, 1u);
+                    table.fail_list[1 + i] = uint32_t(fa);
+                }
+                if (!GS && next < units) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+                return;
+            } else {
+                continue;
+            }
+        }
     }
     if (dbg & 1) return;
 
@@ -1071,7 +1119,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const int start_full = top + kTbWarm;
     const int start = min(start_full, (SPLIT && sp) ? t1s : Tpad);
     // walk starts on the known path (location 0 at and past T)
-    constexpr int kB0 = 32 + kSplitWarm / kChunk;  // frame B's first decoded block (lane)
+    const int kB0 = 32 + warm / kChunk;  // frame B's first decoded block (lane)
     const bool known = (SPLIT && sp) ? (f == 1 && start >= Tb) || (f == 0 && blk >= nA) || (f == 1 && lane < kB0)
                                      : start >= T;
     const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbp) / 48;  // dbg bit 3: warm-up walk only
@@ -1140,7 +1188,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     if (SPLIT && sp) {  // frame A's half up to t1, then frame B's from its step 96
         uint8_t* o = out + fa * out_stride;
         const int na = t1s >> 3;
-        for (int i = lane; i < nbytes; i += 64) o[i] = i < na ? tab[i] : tab[4 * tbb + kSplitWarm / 8 + (i - na)];
+        for (int i = lane; i < nbytes; i += 64) o[i] = i < na ? tab[i] : tab[4 * tbb + warm / 8 + (i - na)];
     } else if (words) {  // lanes 0-31 copy frame A, 32-63 frame B, one dword each per pass
         uint8_t* o = out + (f ? fb : fa) * out_stride;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tab + f * 4 * tbb);
@@ -1156,7 +1204,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     }
     // the prefetched registers are complete before they leave this function (no copy of an
     // in-flight load destination can happen past here)
-    if (LOOP && !GS && next < (frames + 1) / 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+    if (LOOP && !GS && next < units) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
     break;
     }
 }
@@ -1166,13 +1214,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // the dispatcher refilling freed slots unevenly).  !LOOP: one wave per pair, for batches the
 // CUs hold in one round and for the streaming decoder (the loop's extra live state costs
 // ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
-template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false, bool LIST = false>
 __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
                                                     uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {
     static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
-    static_assert(!SPLIT || (!GS && !STREAM && !LOOP), "split frames: LDS survivors, one round");
+    static_assert(!SPLIT || (!GS && !STREAM), "split frames: LDS survivors");
+    if constexpr (LIST) frames = __builtin_amdgcn_readfirstlane(table.fail_list[0]);  // the list's frames
     const size_t pairs = (frames + 1) / 2;
     uint32_t pra = 0, prb = 0;  // next pair's chunk-0 input, prefetched during the traceback (LDS variant)
     uint32_t off[6];
@@ -1186,10 +1235,12 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
         k7_pair<SOFT, GS, STREAM, false, SPLIT>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
                                          ws_wave, sa, blockIdx.x, blockIdx.x, false, pairs, pra, prb, off);
     } else {
-        for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
-            k7_pair<SOFT, GS, STREAM, true, false>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
-                                            ws_wave, sa, wp, blockIdx.x, !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb,
-                                            off);
+        // units: frame pairs, or (SPLIT) frames; every wave leaves the loop when the units run out
+        const size_t units = SPLIT ? frames : pairs;
+        for (size_t wp = blockIdx.x; wp < units; wp += gridDim.x) {
+            k7_pair<SOFT, GS, STREAM, true, SPLIT, false, LIST>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames,
+                                                                dbg, table, ws, ws_wave, sa, wp, blockIdx.x,
+                                                                !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb, off);
             __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
         }
     }
@@ -1424,7 +1475,73 @@ hipError_t launch_k7(const Launch& a) {
     return hipGetLastError();
 }
 
+// Persistent split kernel (frames longer than the LDS variant holds at 8 waves per CU, e.g.
+// config C3's 2,048 bits): one frame per wave as two halves (k7_pair SPLIT), survivors of
+// t1 steps in LDS, frames in a persistent loop; frames whose halves do not converge go to a
+// list that the persistent global-survivor kernel (LIST) decodes afterwards.  The warm-up is
+// 96 steps when 8 waves per CU still fit, else 48.
+bool split_loop_params(const Launch& a, int& warm, size_t& lds) {
+    if (a.S != 6 || a.T < 240) return false;
+    for (int w : {kSplitWarm, kSplitWarm / 2}) {
+        const int t1 = split_t1(a.T, w);
+        if (t1 > 32 * kChunk) return false;  // traceback: at most 32 48-step blocks per half
+        lds = size_t(region0(a.T)) + 16 * size_t(t1);
+        if (lds <= 160 * 1024 / 8) {
+            warm = w;
+            return true;
+        }
+    }
+    return false;
+}
+size_t split_list_bytes(size_t frames) { return (4 * (frames + 1) + 255) / 256 * 256; }
+// waves of the list kernel: what the global variant holds at once for the batch's frame pairs
+size_t list_grid(const Launch& a) { return grid_waves<true>(a); }
+
 }  // namespace
+
+bool k7_split_loop_supported(const Launch& a) {
+    int warm;
+    size_t lds;
+    return split_loop_params(a, warm, lds) && k7_global_supported(a);
+}
+
+size_t k7_split_loop_workspace_bytes(const Launch& a) {
+    return split_list_bytes(a.frames) + list_grid(a) * ws_wave_bytes(a.T);
+}
+
+hipError_t launch_k7_split_loop(const Launch& a) {
+    if (a.frames == 0) return hipSuccess;
+    int warm;
+    size_t lds;
+    if (!a.ws || !split_loop_params(a, warm, lds)) return hipErrorInvalidValue;
+    uint32_t* list = static_cast<uint32_t*>(a.ws);
+    hipError_t e = hipMemsetAsync(list, 0, 4, a.stream);
+    if (e != hipSuccess) return e;
+    Launch la = a;
+    la.split_warm = warm;
+    la.fail_list = list;
+    auto kern = a.soft ? k7_lds_kernel<true, false, false, true, true> : k7_lds_kernel<false, false, false, true, true>;
+    const int per_cu = resident_per_cu(reinterpret_cast<const void*>(kern), lds);
+    size_t grid = size_t(per_cu > 0 ? per_cu : 8) * size_t(a.cus > 0 ? a.cus : 1);
+    if (grid > a.frames) grid = a.frames;
+    hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride, a.T,
+                       a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), la, nullptr, size_t(0),
+                       StreamArgs());
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the frames that did not split: the persistent global-survivor kernel over the list (it
+    // reads the count on the device; with an empty list every wave exits at once)
+    auto lk = a.soft ? k7_lds_kernel<true, true, false, true, false, true> : k7_lds_kernel<false, true, false, true, false, true>;
+    const size_t llds = lds_bytes_gs(a.T, a.soft);
+    if (llds > 64 * 1024) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(lk), hipFuncAttributeMaxDynamicSharedMemorySize, int(llds));
+        if (e != hipSuccess) return e;
+    }
+    la.gs_steps = t_pad(a.T) - gs_lds_steps(a.T, a.soft);
+    hipLaunchKernelGGL(lk, dim3(unsigned(list_grid(a))), dim3(64), llds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
+                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), size_t(0), debug_flags(), la,
+                       static_cast<uint8_t*>(a.ws) + split_list_bytes(a.frames), ws_wave_bytes(a.T), StreamArgs());
+    return hipGetLastError();
+}
 
 bool k7_lds_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes(a.T) <= 160 * 1024; }
 

@@ -18,12 +18,14 @@ from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, nati
 # "auto": the library's own choice; the others force one kernel family: "k7" (K=7,
 # survivors in LDS), "gws" (the same K=7 kernel with survivors in a global workspace), "k9"
 # (K=9, survivors in a global workspace), "lds" (every K).
-KERNELS = ("auto", "k7", "gws", "k9", "lds")
+# "k7s": the K=7 persistent split kernel (one frame per wave as two halves, unconverged frames
+# re-decoded from a list by the global variant) wherever it applies.
+KERNELS = ("auto", "k7", "gws", "k7s", "k9", "lds")
 
 
 class Kern(str):
     def need(self, K):
-        if self in ("k7", "gws") and K != 7:
+        if self in ("k7", "gws", "k7s") and K != 7:
             pytest.skip(f"kernel {self} is K=7 only")
         if self == "k9" and K != 9:
             pytest.skip("kernel k9 is K=9 only")

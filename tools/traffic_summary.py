@@ -27,12 +27,15 @@ with open(os.path.join(repo, "convolutionalencdec_amd", "lib", "libviterbi_amd.s
 
 
 def mean_counter(d, name):
-    vals = []
+    """Counter per decode launch: the mean over dispatches of each decoder kernel, summed over
+    the kernels (a launch may be two dispatches: the persistent split kernel and its list
+    kernel)."""
+    per = {}
     for r in csv.DictReader(open(os.path.join(root, d, "run_counter_collection.csv"))):
         # the decoder's dispatches only (not the device frame generator's or runtime copies)
         if r["Counter_Name"] == name and any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
-            vals.append(float(r["Counter_Value"]))
-    return sum(vals) / len(vals), len(vals)
+            per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return sum(sum(v) / len(v) for v in per.values()), max(len(v) for v in per.values())
 
 
 fetch_kib, nf = mean_counter("pmc_fetch", "FETCH_SIZE")
@@ -61,9 +64,11 @@ if os.path.exists(os.path.join(root, "pmc_valu", "run_counter_collection.csv")):
              "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE")
     v = {n: mean_counter("pmc_valu", n)[0] for n in names}
     kt = os.path.join(root, "pmc_valu", "run_kernel_trace.csv")
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(kt))
-            if "kernel" in r["Kernel_Name"]]
-    dur_ns = sum(durs) / len(durs)
+    durs = {}
+    for r in csv.DictReader(open(kt)):
+        if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
+            durs.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    dur_ns = sum(sum(v) / len(v) for v in durs.values())  # per launch (all its dispatches)
     v["kernel_ns_profiled"] = dur_ns
     v["effective_clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8.0 / dur_ns
     with open(os.path.join(repo, "profiles", rnd, f"pmc_valu_detail_{tag}.json"), "w") as fh:
