@@ -1482,6 +1482,11 @@ hipError_t launch_k7(const Launch& a) {
 // 96 steps when 8 waves per CU still fit, else 48.
 bool split_loop_params(const Launch& a, int& warm, size_t& lds) {
     if (a.S != 6 || a.T < 240) return false;
+    if (const char* v = getenv("VTB_SPLIT_WARM")) {  // measurement only: a fixed warm-up, any occupancy
+        warm = atoi(v) / kChunk * kChunk;
+        lds = size_t(region0(a.T)) + 16 * size_t(split_t1(a.T, warm));
+        return warm >= kChunk && split_t1(a.T, warm) <= 32 * kChunk && lds <= 160 * 1024;
+    }
     for (int w : {kSplitWarm, kSplitWarm / 2}) {
         const int t1 = split_t1(a.T, w);
         if (t1 > 32 * kChunk) return false;  // traceback: at most 32 48-step blocks per half
