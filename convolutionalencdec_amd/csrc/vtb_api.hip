@@ -46,6 +46,9 @@ struct vtb_plan {
     uint8_t* lat_in = nullptr;
     uint8_t* lat_out = nullptr;
     uint32_t* lat_done = nullptr;
+    uint8_t* lat_d_in = nullptr;  // their device addresses (looked up once)
+    uint8_t* lat_d_out = nullptr;
+    uint32_t* lat_d_done = nullptr;
     int seg_waves = 0;  // SEG kernel waves (0: not usable for this plan)
     int seg_warm = 0;
 };
@@ -927,13 +930,14 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");
         plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_out), plan->lat_out, 0) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_done), plan->lat_done, 0) != hipSuccess)
+            return VTB_ERR_DEVICE;
     }
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    uint32_t* d_done = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_in), plan->lat_in, 0) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out), plan->lat_out, 0) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_done), plan->lat_done, 0) != hipSuccess)
-        return VTB_ERR_DEVICE;
+    uint8_t *d_in = plan->lat_d_in, *d_out = plan->lat_d_out;
+    uint32_t* d_done = plan->lat_d_done;
+    if (!d_in || !d_out || !d_done) return VTB_ERR_DEVICE;
     std::memcpy(plan->lat_in, h_in, ib);
     volatile uint32_t* done = plan->lat_done;
     uint32_t status = 0;
