@@ -51,6 +51,8 @@ struct vtb_plan {
     uint32_t* lat_d_done = nullptr;
     int seg_waves = 0;  // SEG kernel waves (0: not usable for this plan)
     int seg_warm = 0;
+    int seg9_wgs = 0;            // K = 9 SEG kernel workgroups (0: not usable for this plan)
+    void* seg9_ws = nullptr;     // its workspace (arrival counter, metrics, survivor words)
 };
 
 // Streaming decoder (include/viterbi_amd.h "Streaming decode"): all streams advance in
@@ -445,6 +447,7 @@ void vtb_plan_destroy(vtb_plan_t* plan) {
         if (plan->lat_out) (void)hipHostFree(plan->lat_out);
         if (plan->lat_done) (void)hipHostFree(plan->lat_done);
     }
+    if (plan->seg9_ws) (void)hipFree(plan->seg9_ws);
     if (plan->ws) {
         (void)hipDeviceSynchronize();  // launches on any stream may still use it
         (void)vtb::workspace_free(plan->ws, nullptr);
@@ -930,6 +933,18 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");
         plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
+        // K = 9: the frame over several workgroups ($VTB_SEG9_WGS: measurement)
+        int wgs = vtb::kSeg9Wgs;
+        if (const char* v = std::getenv("VTB_SEG9_WGS")) wgs = std::atoi(v);
+        if (any && !(vtb::debug_flags() & 1024) && vtb::k9_seg_supported(a, vtb::kSeg9Waves, wgs, vtb::kSeg9Warm)) {
+            const size_t wsb = vtb::k9_seg_workspace_bytes(a, vtb::kSeg9Waves, wgs, vtb::kSeg9Warm);
+            if (hipMalloc(&plan->seg9_ws, wsb) != hipSuccess) {
+                plan->seg9_ws = nullptr;
+                return VTB_ERR_NOMEM;
+            }
+            if (hipMemset(plan->seg9_ws, 0, 256) != hipSuccess) return VTB_ERR_DEVICE;  // the arrival counter
+            plan->seg9_wgs = wgs;
+        }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_out), plan->lat_out, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_done), plan->lat_done, 0) != hipSuccess)
@@ -941,7 +956,7 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
     std::memcpy(plan->lat_in, h_in, ib);
     volatile uint32_t* done = plan->lat_done;
     uint32_t status = 0;
-    if (plan->seg_waves > 0) {
+    if (plan->seg_waves > 0 || plan->seg9_wgs > 0) {
         *done = 0;
         std::atomic_thread_fence(std::memory_order_seq_cst);
         vtb::Launch a;
@@ -957,7 +972,13 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         a.stream = plan->stream;
         a.cus = plan->cus;
         std::memcpy(a.symm, plan->symm, sizeof(a.symm));
-        if (vtb::launch_k7_seg(a, plan->seg_waves, plan->seg_warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+        if (plan->seg_waves > 0) {
+            if (vtb::launch_k7_seg(a, plan->seg_waves, plan->seg_warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+        } else {
+            a.ws = plan->seg9_ws;
+            if (vtb::launch_k9_seg(a, vtb::kSeg9Waves, plan->seg9_wgs, vtb::kSeg9Warm, d_done) != hipSuccess)
+                return VTB_ERR_DEVICE;
+        }
         // wait on the completion word (the kernel's last write); a call that takes longer than
         // ~2 ms (first launch: code-object load) synchronises the stream instead
         const auto t0 = std::chrono::steady_clock::now();

@@ -119,6 +119,14 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s);
 constexpr int kStreamStateWords9 = 260;  // per wave: M[4][64], e[2], flags, pad
 hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s);
 
+// K=9 single-frame latency path (k9_seg_kernel): the frame as segments over `wgs` workgroups
+// of `waves` waves, input staged through LDS, survivors and metrics in a workspace (whose
+// first word, an arrival counter, must be zero before the first launch), *done as for K=7.
+constexpr int kSeg9Waves = 4, kSeg9Wgs = 4, kSeg9Warm = 96;
+bool k9_seg_supported(const Launch& a, int waves, int wgs, int warm);
+size_t k9_seg_workspace_bytes(const Launch& a, int waves, int wgs, int warm);
+hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t* done);
+
 // K=9, survivors in a global workspace (vtb_k9.hip).
 bool k9_supported(const Launch& a);
 size_t k9_workspace_bytes(const Launch& a);

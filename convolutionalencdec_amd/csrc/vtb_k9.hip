@@ -398,8 +398,8 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
 
 // Per register and phase: byte offset of the (V, W) column (edge label c of the butterfly's
 // upper state, R = bit p of the location); the same for every frame pair of the wave.
-__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[4][8]) {
-    const uint32_t lam = lane_of(threadIdx.x);
+__device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[4][8], int lane) {
+    const uint32_t lam = lane_of(uint32_t(lane));
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -415,17 +415,32 @@ __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&o
 // sa.t_end) continue from the metrics in sa.state (delta = 0, Tq = T = the steps received so
 // far), survivor words go to a ring of sa.ring steps (ws_wave = 64 sa.ring bytes per wave), and
 // stream_traceback9 emits the bits that became final.
-template <bool SOFT, bool STREAM = false>
+// SEG (k9_seg_kernel, the single-frame latency path): the waves of several workgroups decode
+// one frame as segments, two per wave in the u16 halves; segment i runs sg->n kernel steps
+// from g_i = i (n - warm), the frame's input is staged in LDS at sg->in_lds, survivor words go
+// to the wave's slot, and the final and warm-up metrics come back in seg_out[0..7].
+struct Seg9 {
+    int n = 0, warm = 0, G = 0;  // steps per segment, warm-up, segments in use
+    int ring_bytes = 0;          // LDS bytes per wave (table ring)
+    int in_lds = 0;              // LDS byte offset of the staged frame
+};
+
+template <bool SOFT, bool STREAM = false, bool SEG = false>
 __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
                                         size_t frames, int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t wp,
-                                        size_t slot, const uint32_t (&off)[4][8], const StreamArgs& sa = StreamArgs()) {
+                                        size_t slot, const uint32_t (&off)[4][8], const StreamArgs& sa = StreamArgs(),
+                                        const Seg9* sg = nullptr, uint32_t* seg_out = nullptr) {
     constexpr uint32_t Q = SOFT ? 255 : 1;
     using H = Hist<SOFT>;
     constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
     extern __shared__ uint4 smem4[];
-    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
-    const int lane = threadIdx.x;
+    const int wv = SEG ? int(threadIdx.x >> 6) : 0;
+    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4) + (SEG ? wv * sg->ring_bytes : 0);
+    const int lane = SEG ? int(threadIdx.x & 63) : int(threadIdx.x);
+    // SEG: this wave's segments (half B a copy of half A when unused) and their first kernel step
+    const int segA = SEG ? 2 * int(slot) : 0, segB = SEG && 2 * int(slot) + 1 < sg->G ? 2 * int(slot) + 1 : segA;
+    const int gA = SEG ? segA * (sg->n - sg->warm) : 0, gB = SEG ? segB * (sg->n - sg->warm) : 0;
     const size_t fa = wp * 2, fb = fa + 1;
     const bool has_b = fb < frames;
     const uint8_t* inA = in + fa * in_stride;
@@ -440,7 +455,19 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         int t = c * kCh + srow - delta;
         t = t < 0 ? 0 : (t < T ? t : T - 1);
-        if constexpr (STREAM) {
+        if constexpr (SEG) {
+            // kernel step g + 48c + r of each half, input step (that - delta), from the LDS copy
+            constexpr int SB = SOFT ? 2 : 1;
+            int ta = gA + c * kCh + srow - delta, tb = gB + c * kCh + srow - delta;
+            ta = ta < 0 ? 0 : (ta < T ? ta : T - 1);
+            tb = tb < 0 ? 0 : (tb < T ? tb : T - 1);
+            const uint32_t la = uint32_t(sg->in_lds + SB * ta), lb = uint32_t(sg->in_lds + SB * tb);
+            if constexpr (SOFT) {
+                asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(ra), "=&v"(rb) : "v"(la), "v"(lb));
+            } else {
+                asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %3" : "=&v"(ra), "=&v"(rb) : "v"(la), "v"(lb));
+            }
+        } else if constexpr (STREAM) {
             // row r of this call: the carry's held-back rows first, then the new input
             constexpr int SB = SOFT ? 2 : 1;
             const int r = t - sa.t_begin;
@@ -478,7 +505,8 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
     };
     // Column k = c + 4R holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
-    const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
+    const uint32_t wbase0 = uint32_t(SEG ? wv * sg->ring_bytes : 0) + 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol,
+                   wbase2 = wbase0 + 48u * kCol;
     auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
@@ -491,6 +519,23 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         // past Tq (W = the metric spread nQS + 1 keeps every survivor at its own location,
         // so the octet that straddles Tq holds the true path's bits; for soft input that W
         // would overflow u16, and the padding survivor bits are overwritten after the ACS).
+        // SEG: per half (kernel steps g + 48c + r).
+        if constexpr (SEG) {
+            const int sa_ = gA + c * kCh + srow, sb_ = gB + c * kCh + srow;
+            const bool ka = sa_ < delta || (!SOFT && sa_ >= Tq), kb = sb_ < delta || (!SOFT && sb_ >= Tq);
+            if (ka || kb) {
+                uint2* col = reinterpret_cast<uint2*>(tab) + srow;
+                constexpr uint32_t PADW = H::SC * ((SOFT ? 2 : 16) * Q + 1) * kR1;
+                const uint32_t keep = (ka ? 0u : 0xFFFFu) | (kb ? 0u : 0xFFFF0000u);
+                const uint32_t tie = et[0] - e[0];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    col[k * kCol] = make_uint2(e[k] & keep, (et[3 - k] & keep) | ((PADW + tie) & ~keep));
+                    col[(4 + k) * kCol] = make_uint2((et[k] & keep) | (tie & ~keep), (e[3 - k] & keep) | (PADW & ~keep));
+                }
+            }
+            return;
+        }
         const bool pad_row = !SOFT && (c + 1) * kCh > Tq && c * kCh + srow >= Tq;
         if ((c == 0 && srow < delta) || pad_row) {
             uint2* col = reinterpret_cast<uint2*>(tab) + srow;
@@ -513,11 +558,16 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
 #pragma unroll
             for (int r = 0; r < 4; r++) M[r] = sa.state[wp * kStreamStateWords9 + 64 * r + lane];
     }
+    if constexpr (SEG) {  // segments after the first start from equal metrics
+#pragma unroll
+        for (int r = 0; r < 4; r++) M[r] = segA > 0 ? B4 * kR1 : (M[r] & 0xFFFFu) | (B4 << 16);
+    }
     uint32_t ra, rb;
     if (!STREAM || Tpad > tbeg) {
         uint32_t e[4], et[4];
         load_raw(tbeg / kCh, ra, rb);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+        if constexpr (SEG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
+        else asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
         stage_compute(ra, rb, e, et);
         stage_write(tbeg / kCh, e, et);
     }
@@ -528,8 +578,8 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         for (int r = 0; r < 4; r++) buf[s][r] = *reinterpret_cast<const uint2*>(tab + off[r][s] + 8 * s);
 
     const uint32_t wlane = 4u * rev6(lam);  // survivor word byte offset of the lane within a column
-    uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4];
-    const int tacs = (dbg & 2) ? 0 : Tpad;
+    uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4], msave[4] = {0, 0, 0, 0};
+    const int tacs = (dbg & 2) ? 0 : SEG ? sg->n : Tpad;
     for (int t0 = tbeg; t0 < tacs; t0 += kCh) {
         const int c0 = t0 / kCh;
         // survivor column of step t0 (streaming: position in the ring)
@@ -539,8 +589,9 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             constexpr int PH = I % 8;
             if constexpr (I == 0) load_raw(c0 + 1, ra, rb);  // next chunk's raw input
             if constexpr (I == 20) {
-                // one survivor store batch (step 15) was issued after the loads
-                asm volatile("s_waitcnt vmcnt(4)" : "+v"(ra), "+v"(rb));
+                // one survivor store batch (step 15) was issued after the loads (SEG: LDS loads)
+                if constexpr (SEG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
+                else asm volatile("s_waitcnt vmcnt(4)" : "+v"(ra), "+v"(rb));
                 stage_compute(ra, rb, se, set);
             }
             if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);  // all rows of this chunk read
@@ -602,8 +653,47 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                 }
             }
         });
+        if constexpr (SEG) {
+            if (t0 == sg->warm - kCh)
+#pragma unroll
+                for (int r = 0; r < 4; r++) msave[r] = M[r];
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if constexpr (SEG) {
+        // soft input: the last segment's padding steps (kernel steps >= Tq) get own-keeping
+        // survivor bits, one bit per step, in that segment's half of the words
+        if (SOFT && !(dbg & 2)) {
+            uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + slot * ws_wave);
+            for (int h = 0; h < 2; h++) {
+                const int g0 = h ? gB : gA;
+                if (h == 1 && segB == segA) break;
+                const int lo = Tq - g0;  // first local padding step
+                if (lo >= sg->n) continue;
+                for (int g = (lo > 0 ? lo : 0) >> 4; g < (sg->n >> 4); g++) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t lp = (rev6(lam) << 2) | uint32_t(rev2(r));
+                        uint32_t own = 0, mask = 0;
+                        for (int t = (16 * g > lo ? 16 * g : lo); t < 16 * g + 16; t++) {
+                            const int w = (t & 15) >> 1, bit = 8 * (w & 1) + 2 * (w >> 1) + (t & 1);
+                            own |= ((lp >> ((g0 + t) & 7)) & 1u) << bit;
+                            mask |= 1u << bit;
+                        }
+                        own <<= 16 * h;
+                        mask <<= 16 * h;
+                        uint32_t* p = wsw + (kColBytes / 4) * g + (wlane >> 2) + 64 * rev2(r);
+                        *p = (*p & ~mask) | (own & mask);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) seg_out[r] = M[r], seg_out[4 + r] = msave[r];
+        return;
+    }
 
     if constexpr (STREAM) {
         if (!sa.last)
@@ -716,6 +806,164 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     }
 }
 
+// Single-frame latency path for K = 9 (vtb_decode_frame_sync): the frame is cut into up to
+// 2 x waves segments over several workgroups of W waves (one per SIMD), each workgroup
+// stages the whole frame from (host-mapped) memory into LDS once, every wave runs the ACS of
+// its two segments (k9_pair SEG, survivor words in its workspace slot) and publishes its
+// final and warm-up metric vectors; the last workgroup to arrive (atomic counter) checks
+// every segment boundary (metrics equal up to a constant, vtb_k7_lds.hip §SEG), and its wave 0
+// traces the frame back over all segments' words and writes the bytes, then *done = 1 (2: a
+// boundary did not converge, nothing written: the caller decodes the frame whole).
+struct Seg9Args {
+    Seg9 s;
+    uint32_t* met;      // per global wave: final [4][64], warm-up [4][64] (packed pairs)
+    uint32_t* counter;  // workgroups arrived; the last one resets it
+    uint32_t* done;     // completion word (host-mapped) or null
+    int nwg;            // workgroups
+    int ob_lds;         // LDS byte offset of the decoded bytes
+    int flag_lds;       // LDS byte offset of the election flag and the per-wave check results
+    int xcd;            // grid stride of the working workgroups (8: all on one XCD, one L2)
+};
+
+template <bool SOFT>
+__global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int T,
+                                                     int L, int delta, int Tq, int dbg, Launch table,
+                                                     uint8_t* __restrict__ ws, size_t ws_wave, Seg9Args a) {
+    extern __shared__ uint4 smem4[];
+    uint8_t* sm = reinterpret_cast<uint8_t*>(smem4);
+    if (int(blockIdx.x) % a.xcd) return;  // placeholder workgroups of the XCD-local grid
+    const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63), W = int(blockDim.x >> 6);
+    const int gw = int(blockIdx.x) / a.xcd * W + wv;  // global wave: segments 2gw, 2gw + 1
+    {
+        // the frame into LDS: up to four 16-byte loads per thread, all issued before any store
+        const int nin = (SOFT ? 2 : 1) * T, step = 16 * int(blockDim.x), i0 = 16 * int(threadIdx.x);
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
+        if (i0 < nin) v0 = *reinterpret_cast<const uint4*>(in + i0);
+        if (i0 + step < nin) v1 = *reinterpret_cast<const uint4*>(in + i0 + step);
+        if (i0 + 2 * step < nin) v2 = *reinterpret_cast<const uint4*>(in + i0 + 2 * step);
+        if (i0 + 3 * step < nin) v3 = *reinterpret_cast<const uint4*>(in + i0 + 3 * step);
+        uint8_t* dst = sm + a.s.in_lds + i0;
+        if (i0 < nin) *reinterpret_cast<uint4*>(dst) = v0;
+        if (i0 + step < nin) *reinterpret_cast<uint4*>(dst + step) = v1;
+        if (i0 + 2 * step < nin) *reinterpret_cast<uint4*>(dst + 2 * step) = v2;
+        if (i0 + 3 * step < nin) *reinterpret_cast<uint4*>(dst + 3 * step) = v3;
+    }
+    __syncthreads();
+    const int G = a.s.G;
+    if (2 * gw < G) {
+        uint32_t off[4][8];
+        column_offsets(table, off, lane);
+        uint32_t fm[8];
+        k9_pair<SOFT, false, true>(in, 0, out, 0, T, L, delta, Tq, 0, 0, 1, dbg, ws, ws_wave, 0, size_t(gw), off,
+                                   StreamArgs(), &a.s, fm);
+        uint32_t* mw = a.met + size_t(gw) * 512;
+#pragma unroll
+        for (int r = 0; r < 4; r++) mw[64 * r + lane] = fm[r], mw[256 + 64 * r + lane] = fm[4 + r];
+    }
+    // the last workgroup to arrive does the rest (release: this workgroup's words and metrics)
+    uint32_t* flag = reinterpret_cast<uint32_t*>(sm + a.flag_lds);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) flag[0] = atomicAdd(a.counter, 1u) == uint32_t(a.nwg - 1) ? 1u : 0u;
+    __syncthreads();
+    if (flag[0] == 0u) return;  // (the whole workgroup: no barrier follows for it)
+    __threadfence();            // acquire: every workgroup's words and metrics
+    // boundaries i = 1 .. G-1: segment i's metrics at the end of its warm-up against segment
+    // i - 1's final metrics (the same step), equal up to a constant over all 256 states
+    using H = Hist<SOFT>;
+    constexpr uint32_t KEEP = 0xFFFFu & ~(H::SC - 1);
+    bool ok = true;
+    for (int i = 1 + wv; i < G; i += W) {
+        const uint32_t* pf = a.met + size_t((i - 1) >> 1) * 512;        // segment i - 1: final
+        const uint32_t* pw = a.met + size_t(i >> 1) * 512 + 256;        // segment i: warm-up end
+        const int sf = 16 * ((i - 1) & 1), sw = 16 * (i & 1);
+        uint32_t x[4], y[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) x[r] = (pf[64 * r + lane] >> sf) & KEEP, y[r] = (pw[64 * r + lane] >> sw) & KEEP;
+        const uint32_t x0 = __builtin_amdgcn_readfirstlane(x[0]), y0 = __builtin_amdgcn_readfirstlane(y[0]);
+        bool same = true;
+#pragma unroll
+        for (int r = 0; r < 4; r++) same = same && ((x[r] - x0) & 0xFFFFu) == ((y[r] - y0) & 0xFFFFu);
+        ok = ok && __ballot(same) == ~0ull;
+    }
+    if (lane == 0) flag[1 + wv] = ok ? 1u : 0u;
+    __syncthreads();
+    bool all = true;
+    for (int i = 0; i < W; i++) all = all && flag[1 + i] != 0u;
+    if (dbg & 2) all = true;  // (VTB_DEBUG 2, 1: no ACS / no traceback, phase timing only)
+    if (wv != 0) return;
+    if (lane == 0) *a.counter = 0u;  // for the next launch (stream-ordered after this one)
+    if (dbg & 1) {
+        if (a.done && lane == 0) __hip_atomic_store(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (!all) {
+        if (a.done && lane == 0) __hip_atomic_store(a.done, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    // traceback, wave 0: blocks of tbp kernel steps (a multiple of 48), lane b = block b; the
+    // 48 steps at tlo read the words of the segment that owns them (one workspace for all
+    // segments: slot * ws_wave is a multiple of the 1-KB column, so the in-place address edits
+    // of tb_body stay inside the column)
+    const int n = a.s.n, warm = a.s.warm, stp = n - warm, Tpad = (Tq + kCh - 1) / kCh * kCh;
+    const uint64_t gbase = uniform64(reinterpret_cast<uint64_t>(ws));
+    auto col_at = [&](int tlo) -> uint32_t {
+        int i = tlo < warm ? 0 : (tlo - warm) / stp;
+        if (i > G - 1) i = G - 1;
+        const int lt = tlo - i * stp;
+        return uint32_t(size_t(i >> 1) * ws_wave) + uint32_t(2 * (i & 1)) + uint32_t(kColBytes * (lt >> 4));
+    };
+    auto tb48 = [&](uint32_t cb, uint32_t& la) {
+        if constexpr (SOFT) return tb_body(cb, la, gbase);
+        else return tb_body8(cb, la, gbase);
+    };
+    uint8_t* ob = sm + a.ob_lds;
+    const int nb48 = Tpad / kCh;
+    const int tbp = (nb48 + 63) / 64 * kCh;
+    const bool active = lane * tbp < Tpad;
+    const int start_full = (lane + 1) * tbp + kTbWarm;
+    const int start = min(start_full, Tpad);
+    const bool known = start >= Tq;
+    const int nbody = (kTbWarm + tbp) / 48;
+    uint32_t loc = 0, loc_top = 0;
+    if (active) {
+        for (int g = 0; g < nbody; g++) {
+            const int tlo = start_full - 48 * (g + 1);
+            if (g == kTbWarm / 48) loc_top = loc;
+            if (tlo < start) {
+                const uint64_t bits = tb48(col_at(tlo), loc);
+                if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
+            }
+        }
+    }
+    uint32_t fin = loc;
+    bool fixed = known || !active;
+    for (int round = 0; round < 65; round++) {
+        const uint32_t sfin = __shfl_down(fin, 1);
+        const bool okb = fixed || loc_top == sfin;
+        const uint64_t bad = ~__ballot(okb);
+        if (bad == 0) break;
+        if (!okb && (bad >> (lane + 1)) == 0) {
+            loc = sfin;
+            for (int g = kTbWarm / 48; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                put_bits48(ob, tlo, tb48(col_at(tlo), loc));
+            }
+            fin = loc;
+            fixed = true;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // copy out; with delta = 1 kernel step t' is input step t' - 1 (shift the stream one bit)
+    const int nbytes = (L + 7) >> 3;
+    for (int j = lane; j < nbytes; j += 64) out[j] = delta ? uint8_t((ob[j] << 1) | (ob[j + 1] >> 7)) : ob[j];
+    if (a.done) {
+        __threadfence_system();
+        if (lane == 0) __hip_atomic_store(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // LOOP: persistent over frame pairs (as vtb_k7_lds.hip), wave b decodes pairs b, b + grid, ...;
 // !LOOP: one wave per pair, for batches the CUs hold in one round (fewer live registers).
 template <bool SOFT, bool LOOP, bool STREAM = false>
@@ -725,7 +973,7 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
                                                 uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa = StreamArgs()) {
     static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
     uint32_t off[4][8];
-    column_offsets(table, off);
+    column_offsets(table, off, threadIdx.x);
     if constexpr (STREAM) {
         k9_pair<SOFT, true>(in, in_stride, out, out_stride, T, L, 0, T, Tpad, 0, frames, dbg, ws, ws_wave, blockIdx.x,
                             blockIdx.x, off, sa);
@@ -759,7 +1007,77 @@ size_t grid_waves(const Launch& a, int Tq) {
     return cap < grid ? cap : grid;
 }
 
+// K = 9 single-frame geometry: W waves per workgroup, up to `wgs` workgroups; n = ACS steps per
+// segment (multiple of 48) so that 2 W wgs segments cover Tq, G = the segments whose exact part
+// starts before Tq.
+bool k9_seg_geometry(int Tq, int W, int wgs, int warm, Seg9& sg, int& nwg) {
+    if (W < 1 || W > 4 || wgs < 1 || wgs > 64 || warm < kCh || warm % kCh) return false;
+    const int G2 = 2 * W * wgs;
+    int n = (Tq + (G2 - 1) * warm + G2 - 1) / G2;
+    n = (n + kCh - 1) / kCh * kCh;
+    if (n < warm + kCh) n = warm + kCh;
+    int G = 1;
+    while (G < G2 && G * (n - warm) + warm < Tq) G++;
+    if ((G - 1) * (n - warm) + n < Tq) return false;
+    sg.n = n, sg.warm = warm, sg.G = G;
+    nwg = ((G + 1) / 2 + W - 1) / W;
+    return true;
+}
+
+size_t k9_seg_lds(int T, int Tq, bool soft, int W, int& in_lds, int& ob_lds, int& flag_lds) {
+    in_lds = W * ((kRingBytes + 15) / 16 * 16);
+    ob_lds = in_lds + ((soft ? 2 : 1) * T + 15) / 16 * 16;
+    flag_lds = ob_lds + (t_pad(Tq) / 8 + 16 + 15) / 16 * 16;
+    return size_t(flag_lds) + 4 * (1 + W);
+}
 }  // namespace
+
+bool k9_seg_supported(const Launch& a, int waves, int wgs, int warm) {
+    const int delta = a.T & 1, Tq = a.T + delta;
+    Seg9 sg;
+    int nwg, il, ol, fl;
+    if (a.S != 8 || a.T < 240 || !k9_seg_geometry(Tq, waves, wgs, warm, sg, nwg)) return false;
+    const int nin = (a.soft ? 2 : 1) * a.T;
+    return nin <= 16 * 4 * 64 * waves && k9_seg_lds(a.T, Tq, a.soft, waves, il, ol, fl) <= 64 * 1024;
+}
+
+size_t k9_seg_workspace_bytes(const Launch& a, int waves, int wgs, int warm) {
+    const int Tq = a.T + (a.T & 1);
+    Seg9 sg;
+    int nwg;
+    if (!k9_seg_geometry(Tq, waves, wgs, warm, sg, nwg)) return 0;
+    const size_t nw = size_t(nwg) * waves;
+    return 256 + nw * 512 * 4 + nw * size_t(kColBytes) * (sg.n / 16);  // counter, metrics, words
+}
+
+hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t* done) {
+    const int delta = a.T & 1, Tq = a.T + delta;
+    Seg9Args g;
+    int nwg;
+    if (!a.ws || !k9_seg_geometry(Tq, waves, wgs, warm, g.s, nwg)) return hipErrorInvalidValue;
+    int il, ol, fl;
+    const size_t lds = k9_seg_lds(a.T, Tq, a.soft, waves, il, ol, fl);
+    g.s.ring_bytes = (kRingBytes + 15) / 16 * 16;
+    g.s.in_lds = il;
+    g.ob_lds = ol;
+    g.flag_lds = fl;
+    g.nwg = nwg;
+    g.done = done;
+    // all working workgroups on one XCD (workgroups go round-robin over the 8 XCDs): the
+    // arrival fences and the traceback's word reads stay within one L2 (72.7 against 67.4
+    // Mbit/s for speedDecode K=9); $VTB_SEG9_XCD=0 spreads them (measurement)
+    g.xcd = 8;
+    if (const char* v = std::getenv("VTB_SEG9_XCD")) g.xcd = std::atoi(v) > 0 ? 8 : 1;
+    uint8_t* base = static_cast<uint8_t*>(a.ws);
+    g.counter = reinterpret_cast<uint32_t*>(base);
+    g.met = reinterpret_cast<uint32_t*>(base + 256);
+    const size_t nw = size_t(nwg) * waves, ws_wave = size_t(kColBytes) * (g.s.n / 16);
+    uint8_t* words = base + 256 + nw * 512 * 4;
+    auto kern = a.soft ? k9_seg_kernel<true> : k9_seg_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3(unsigned(nwg * g.xcd)), dim3(64 * waves), lds, a.stream, a.in, a.out, a.T, a.L, delta, Tq,
+                       debug_flags(), a, words, ws_wave, g);
+    return hipGetLastError();
+}
 
 bool k9_supported(const Launch& a) {
     return a.S == 8 && a.T > a.S && (size_t)region0(a.T + (a.T & 1)) <= 160 * 1024;

@@ -14,4 +14,12 @@ oracle/_ref/speedDecode_amd > gpurun_out/speedDecode_amd.log 2>&1 &
 pid=$!; sleep $((secs + 4)); kill $pid; wait $pid 2>/dev/null
 grep -h "Rate" gpurun_out/speedDecode_ref.log | tail -3 | sed 's/^/ref: /'
 grep -h "Rate" gpurun_out/speedDecode_amd.log | tail -3 | sed 's/^/amd: /'
+if [ "$2" = k9 ]; then  # the K=9 configuration (params/k9)
+  oracle/_ref/speedDecode_ref_k9 > gpurun_out/speedDecode_ref_k9.log 2>&1 &
+  pid=$!; sleep $secs; kill $pid; wait $pid 2>/dev/null
+  oracle/_ref/speedDecode_amd_k9 > gpurun_out/speedDecode_amd_k9.log 2>&1 &
+  pid=$!; sleep $((secs + 4)); kill $pid; wait $pid 2>/dev/null
+  grep -h "Rate" gpurun_out/speedDecode_ref_k9.log | tail -3 | sed 's/^/ref K=9: /'
+  grep -h "Rate" gpurun_out/speedDecode_amd_k9.log | tail -3 | sed 's/^/amd K=9: /'
+fi
 exit 0
