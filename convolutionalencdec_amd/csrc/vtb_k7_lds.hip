@@ -1387,7 +1387,9 @@ __global__ __launch_bounds__(256) void k7_seg_kernel(const uint8_t* __restrict__
         for (int i = lane; i < nbytes; i += 64) o[i] = ob[i];
     }
     if (sg.done) {
-        __threadfence_system();
+        // every lane's output stores complete, then the system-scope release store (its
+        // own fence writes back; no acquire needed here, so no __threadfence_system)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(sg.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }

@@ -104,10 +104,24 @@ __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b
     return r;
 }
 
-// One coalesced wave store of survivor words (saddr form: wave base in SGPRs).
-template <int OFF>
+// One coalesced wave store of survivor words (saddr form: wave base in SGPRs); SC: write-through
+// (sc1), the words another workgroup reads in the same launch (k9_seg_kernel).
+template <int OFF, bool SC = false>
 __device__ __forceinline__ void gstore(uint32_t vo, uint32_t z, uint64_t base) {
-    asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+    if constexpr (SC)
+        asm volatile("global_store_dword %0, %1, %2 offset:%3 sc1" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+    else
+        asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+}
+
+// Words handed from one workgroup to another inside a launch: global (never flat) agent-scope
+// relaxed accesses, i.e. sc1 stores and loads that bypass the per-CU L1.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load((const gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int... Is, class F>
@@ -165,6 +179,7 @@ __device__ __forceinline__ uint32_t lprime_of(uint32_t a) { return (a & 0xFCu) |
 // 48 traceback steps over [tlo, tlo + 48), newest first (see vtb_k7_lds.hip tb_body).  cb is
 // the byte offset of the block's first survivor column plus 2f (bits 2..9 clear); la the
 // address field of the survivor's location.  Returns the 48 decoded bits, bit 0 = step tlo.
+template <bool SC = false>
 __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t gbase) {
     uint32_t a = cb | la;
     uint64_t bits = 0;
@@ -203,8 +218,12 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t 
         if (j % 4 == 0) bits |= uint64_t(lprime_of(a)) << (8 * (5 - j / 4));  // octet ending at tlo + todd + 1
         const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
         uint32_t v;
-        asm volatile("global_load_ushort %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
-                     : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * kColBytes));
+        if constexpr (SC)
+            asm volatile("global_load_ushort %0, %1, %2 offset:%3 sc1\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * kColBytes));
+        else
+            asm volatile("global_load_ushort %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * kColBytes));
         const int pos = addr_pos((todd - 1) & 7);
         const uint32_t fld = pos >= sh ? (v << (pos - sh)) : (v >> (sh - pos));
         a = (a & ~(3u << pos)) | (fld & (3u << pos));
@@ -217,6 +236,7 @@ __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t 
 // (steps tlo + 8k + b) at the survivor's location holds the decisions D_b along its path, and
 // D_b is l' bit b (step t's pairing bit is bit t mod 8 of l'), so the location eight steps
 // back is the byte itself and the octet's eight decoded bits are its end location l'.
+template <bool SC = false>
 __device__ __forceinline__ uint64_t tb_body8(uint32_t cb, uint32_t& la, uint64_t gbase) {
     uint32_t a = cb | la;
     uint64_t bits = 0;
@@ -224,8 +244,12 @@ __device__ __forceinline__ uint64_t tb_body8(uint32_t cb, uint32_t& la, uint64_t
     for (int k = 5; k >= 0; k--) {
         bits |= uint64_t(lprime_of(a)) << (8 * k);
         uint32_t v;
-        asm volatile("global_load_ubyte %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
-                     : "=v"(v) : "v"(a), "s"(gbase), "i"(kColBytes * (k >> 1) + (k & 1)));
+        if constexpr (SC)
+            asm volatile("global_load_ubyte %0, %1, %2 offset:%3 sc1\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"(kColBytes * (k >> 1) + (k & 1)));
+        else
+            asm volatile("global_load_ubyte %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"(kColBytes * (k >> 1) + (k & 1)));
         a = (a & ~0x3FCu) | (v & 0xFCu) | ((v & 3u) << 8);
     }
     la = a & 0x3FCu;
@@ -623,10 +647,10 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                 }
                 if constexpr ((I & 15) == 15) {
                     constexpr int W = I >> 4;
-                    gstore<W * kColBytes + 256 * rev2(0)>(gvo, pw[0][0], gbase);
-                    gstore<W * kColBytes + 256 * rev2(1)>(gvo, pw[1][0], gbase);
-                    gstore<W * kColBytes + 256 * rev2(2)>(gvo, pw[2][0], gbase);
-                    gstore<W * kColBytes + 256 * rev2(3)>(gvo, pw[3][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(0), SEG>(gvo, pw[0][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(1), SEG>(gvo, pw[1][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(2), SEG>(gvo, pw[2][0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(3), SEG>(gvo, pw[3][0], gbase);
                 }
             }
             if constexpr (SOFT && (I & 1)) {
@@ -646,10 +670,10 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                         z[r] = bfi_op(0x0F0F0F0Fu, z[r], pw[r][2] << 4);
                         z[r] = bfi_op(0x3F3F3F3Fu, z[r], pw[r][3] << 6);
                     }
-                    gstore<W * kColBytes + 256 * rev2(0)>(gvo, z[0], gbase);
-                    gstore<W * kColBytes + 256 * rev2(1)>(gvo, z[1], gbase);
-                    gstore<W * kColBytes + 256 * rev2(2)>(gvo, z[2], gbase);
-                    gstore<W * kColBytes + 256 * rev2(3)>(gvo, z[3], gbase);
+                    gstore<W * kColBytes + 256 * rev2(0), SEG>(gvo, z[0], gbase);
+                    gstore<W * kColBytes + 256 * rev2(1), SEG>(gvo, z[1], gbase);
+                    gstore<W * kColBytes + 256 * rev2(2), SEG>(gvo, z[2], gbase);
+                    gstore<W * kColBytes + 256 * rev2(3), SEG>(gvo, z[3], gbase);
                 }
             }
         });
@@ -684,7 +708,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                         own <<= 16 * h;
                         mask <<= 16 * h;
                         uint32_t* p = wsw + (kColBytes / 4) * g + (wlane >> 2) + 64 * rev2(r);
-                        *p = (*p & ~mask) | (own & mask);
+                        st_agent(p, (ld_agent(p) & ~mask) | (own & mask));
                     }
                 }
             }
@@ -858,16 +882,21 @@ __global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__
                                    StreamArgs(), &a.s, fm);
         uint32_t* mw = a.met + size_t(gw) * 512;
 #pragma unroll
-        for (int r = 0; r < 4; r++) mw[64 * r + lane] = fm[r], mw[256 + 64 * r + lane] = fm[4 + r];
+        for (int r = 0; r < 4; r++) st_agent(mw + 64 * r + lane, fm[r]), st_agent(mw + 256 + 64 * r + lane, fm[4 + r]);
     }
-    // the last workgroup to arrive does the rest (release: this workgroup's words and metrics)
+    // the last workgroup to arrive does the rest.  Hand-off (cdna_hip_programming.md Guideline
+    // 16, write-through form): every word another workgroup reads (survivor words, metrics) is
+    // stored sc1 and drained by its wave before the barrier, one lane adds to the counter, and
+    // every load of those words in the last workgroup is an sc1 load (no fences)
     uint32_t* flag = reinterpret_cast<uint32_t*>(sm + a.flag_lds);
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) flag[0] = atomicAdd(a.counter, 1u) == uint32_t(a.nwg - 1) ? 1u : 0u;
+    if (threadIdx.x == 0)
+        flag[0] = __hip_atomic_fetch_add((gu32*)(a.counter), 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == uint32_t(a.nwg - 1) ? 1u : 0u;
     __syncthreads();
     if (flag[0] == 0u) return;  // (the whole workgroup: no barrier follows for it)
-    __threadfence();            // acquire: every workgroup's words and metrics
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (orders the loads after the election)
     // boundaries i = 1 .. G-1: segment i's metrics at the end of its warm-up against segment
     // i - 1's final metrics (the same step), equal up to a constant over all 256 states
     using H = Hist<SOFT>;
@@ -879,7 +908,7 @@ __global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__
         const int sf = 16 * ((i - 1) & 1), sw = 16 * (i & 1);
         uint32_t x[4], y[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) x[r] = (pf[64 * r + lane] >> sf) & KEEP, y[r] = (pw[64 * r + lane] >> sw) & KEEP;
+        for (int r = 0; r < 4; r++) x[r] = (ld_agent(pf + 64 * r + lane) >> sf) & KEEP, y[r] = (ld_agent(pw + 64 * r + lane) >> sw) & KEEP;
         const uint32_t x0 = __builtin_amdgcn_readfirstlane(x[0]), y0 = __builtin_amdgcn_readfirstlane(y[0]);
         bool same = true;
 #pragma unroll
@@ -892,7 +921,7 @@ __global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__
     for (int i = 0; i < W; i++) all = all && flag[1 + i] != 0u;
     if (dbg & 2) all = true;  // (VTB_DEBUG 2, 1: no ACS / no traceback, phase timing only)
     if (wv != 0) return;
-    if (lane == 0) *a.counter = 0u;  // for the next launch (stream-ordered after this one)
+    if (lane == 0) st_agent(a.counter, 0u);  // for the next launch (stream-ordered after this one)
     if (dbg & 1) {
         if (a.done && lane == 0) __hip_atomic_store(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
@@ -914,8 +943,8 @@ __global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__
         return uint32_t(size_t(i >> 1) * ws_wave) + uint32_t(2 * (i & 1)) + uint32_t(kColBytes * (lt >> 4));
     };
     auto tb48 = [&](uint32_t cb, uint32_t& la) {
-        if constexpr (SOFT) return tb_body(cb, la, gbase);
-        else return tb_body8(cb, la, gbase);
+        if constexpr (SOFT) return tb_body<true>(cb, la, gbase);
+        else return tb_body8<true>(cb, la, gbase);
     };
     uint8_t* ob = sm + a.ob_lds;
     const int nb48 = Tpad / kCh;
@@ -959,7 +988,9 @@ __global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__
     const int nbytes = (L + 7) >> 3;
     for (int j = lane; j < nbytes; j += 64) out[j] = delta ? uint8_t((ob[j] << 1) | (ob[j + 1] >> 7)) : ob[j];
     if (a.done) {
-        __threadfence_system();
+        // every lane's output stores complete, then the system-scope release store (its
+        // own fence writes back; no acquire needed here, so no __threadfence_system)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
