@@ -80,31 +80,36 @@ def test_random_case_vs_oracle(orc, case):
     assert bad.size == 0, (case, bad.size, bad[:8])
 
 
-def _frame_cases(n=48, seed=20261017):
+def _frame_cases(n=72, seed=20261017):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
+        K = 9 if i % 3 == 2 else 7
         soft = bool(rng.integers(0, 2))
         L = int(rng.integers(1, 4090 if soft else 8100))
+        if K == 9 and L > 12000:
+            L = 12000
         noise = float(rng.choice([0.0, 0.03, 0.07, 0.5]))
-        out.append((i, L, soft, noise))
+        out.append((i, L, soft, noise, K))
     return out
 
 
-@pytest.mark.parametrize("case", _frame_cases(), ids=lambda c: f"{c[0]}-L{c[1]}-{'soft' if c[2] else 'hard'}-p{c[3]}")
+@pytest.mark.parametrize("case", _frame_cases(),
+                         ids=lambda c: f"{c[0]}-K{c[4]}-L{c[1]}-{'soft' if c[2] else 'hard'}-p{c[3]}")
 def test_single_frame_path_vs_oracle(orc, case, monkeypatch):
-    """vtb_decode_frame_sync (the segmented single-frame kernel, or its frame-kernel fallback
-    when a segment has not converged) at random frame lengths and noise levels."""
+    """vtb_decode_frame_sync (the segmented single-frame kernels, K=7 on one workgroup and K=9
+    over several, or the frame-kernel fallback when a segment has not converged) at random
+    frame lengths and noise levels."""
     monkeypatch.delenv("VTB_KERNEL", raising=False)
-    i, L, soft, noise = case
+    i, L, soft, noise, K = case
     if soft:
         sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
-        unc, x = random_frames(orc, 7, L, 3, 0.0, 5000 + i, soft=True, sigma=sigma)
+        unc, x = random_frames(orc, K, L, 3, 0.0, 5000 + i, soft=True, sigma=sigma)
     else:
-        unc, x = random_frames(orc, 7, L, 3, noise, 5000 + i)
+        unc, x = random_frames(orc, K, L, 3, noise, 5000 + i)
     x = np.ascontiguousarray(x).reshape(3, -1)
-    want = orc.decode(7, CODES[7], x, L, soft=soft, threads=THREADS)
-    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L, soft=soft)
+    want = orc.decode(K, CODES[K], x, L, soft=soft, threads=THREADS)
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
     got = np.stack([d.decode_frame(r) for r in x])
     assert (got == want).all(), case
 
