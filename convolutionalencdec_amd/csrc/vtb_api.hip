@@ -921,8 +921,12 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         }
         std::memset(plan->lat_in, 0, (ib + 32) / 16 * 16);
         // SEG kernel geometry, read once per plan ($VTB_SEG_WAVES / $VTB_SEG_WARM: measurement)
-        int waves = 4, warm = vtb::kSegWarm;
-        if (const char* v = std::getenv("VTB_SEG_WAVES")) waves = std::atoi(v);
+        // eight waves (two per SIMD, 16 segments: 128.5 against 120 Mbit/s for four in the
+        // reference's speedDecode); four where eight waves' survivor words do not
+        // fit the CU's LDS (frames past about 12,000 bits)
+        int waves = 8, warm = vtb::kSegWarm;
+        const char* wenv = std::getenv("VTB_SEG_WAVES");
+        if (wenv) waves = std::atoi(wenv);
         if (const char* v = std::getenv("VTB_SEG_WARM")) warm = std::atoi(v);
         vtb::Launch a;
         a.S = plan->code.constraint_length - 1;
@@ -931,6 +935,7 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         a.L = plan->L;
         const char* force = std::getenv("VTB_KERNEL");
         const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");
+        if (!wenv && !vtb::k7_seg_supported(a, waves, warm)) waves = 4;
         plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
         // K = 9: the frame over several workgroups ($VTB_SEG9_WGS: measurement)

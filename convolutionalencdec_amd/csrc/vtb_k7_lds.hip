@@ -1271,7 +1271,7 @@ __global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ 
 // system-scope release, so a host thread can wait on it instead of synchronising the stream.
 constexpr int kSegLoads = 4;  // 16-byte staging loads per thread: frames of up to 64 B per thread
 template <bool SOFT>
-__global__ __launch_bounds__(256) void k7_seg_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+__global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                      uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                      int Tpad, int r0, int dbg, Launch table, SegArgs sg) {
     extern __shared__ uint4 smem4[];
@@ -1566,7 +1566,7 @@ hipError_t launch_k7_global(const Launch& a) { return launch_k7<true>(a); }
 // segment (multiple of 48) with 2W segments covering T, G = the segments whose exact region
 // [s_i, s_i+1) starts before T.
 bool k7_seg_geometry(int T, int W, int warm, SegArgs& sg) {
-    if (W < 1 || W > 4 || warm < 48 || warm % 48) return false;
+    if (W < 1 || W > 8 || warm < 48 || warm % 48) return false;
     const int G2 = 2 * W;
     int n = (T + (G2 - 1) * warm + G2 - 1) / G2;
     n = (n + kChunk - 1) / kChunk * kChunk;

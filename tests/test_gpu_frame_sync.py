@@ -52,7 +52,7 @@ def test_golden_vectors_k7(monkeypatch):
     assert s1[0] > s0[0], (s0, s1)  # the segmented kernel ran (frames of T >= 240)
 
 
-@pytest.mark.parametrize("L", [234, 300, 1000, 1024, 2048, 2049, 3000, 4090, 8000])
+@pytest.mark.parametrize("L", [234, 300, 1000, 1024, 2048, 2049, 3000, 4090, 8000, 12000, 16384])
 @pytest.mark.parametrize("soft", [False, True])
 def test_random_vs_oracle(orc, L, soft, monkeypatch):
     monkeypatch.delenv("VTB_KERNEL", raising=False)
@@ -67,10 +67,11 @@ def test_random_vs_oracle(orc, L, soft, monkeypatch):
     got = run(d, rx)
     s1 = seg_stats()
     assert (got == want).all()
-    assert s1[0] - s0[0] >= F // 2, (s0, s1)  # these noise levels mostly converge within the warm-up
+    if L <= 8000:  # (longer frames: the frame kernel where the segments' words exceed the LDS)
+        assert s1[0] - s0[0] >= F // 2, (s0, s1)  # these noise levels mostly converge within the warm-up
 
 
-@pytest.mark.parametrize("waves", [1, 2, 3])
+@pytest.mark.parametrize("waves", [1, 2, 3, 4, 5, 7])
 def test_fewer_waves(orc, waves, monkeypatch):
     monkeypatch.delenv("VTB_KERNEL", raising=False)
     monkeypatch.setenv("VTB_SEG_WAVES", str(waves))
