@@ -52,6 +52,7 @@ struct vtb_plan {
     int seg_waves = 0;  // SEG kernel waves (0: not usable for this plan)
     int seg_warm = 0;
     int seg9_wgs = 0;            // K = 9 SEG kernel workgroups (0: not usable for this plan)
+    int seg9_waves = 0;          // and waves per workgroup
     void* seg9_ws = nullptr;     // its workspace (arrival counter, metrics, survivor words)
 };
 
@@ -939,16 +940,18 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
         // K = 9: the frame over several workgroups ($VTB_SEG9_WGS: measurement)
-        int wgs = vtb::kSeg9Wgs;
+        int wgs = vtb::kSeg9Wgs, w9 = vtb::kSeg9Waves;
         if (const char* v = std::getenv("VTB_SEG9_WGS")) wgs = std::atoi(v);
-        if (any && !(vtb::debug_flags() & 1024) && vtb::k9_seg_supported(a, vtb::kSeg9Waves, wgs, vtb::kSeg9Warm)) {
-            const size_t wsb = vtb::k9_seg_workspace_bytes(a, vtb::kSeg9Waves, wgs, vtb::kSeg9Warm);
+        if (const char* v = std::getenv("VTB_SEG9_WAVES")) w9 = std::atoi(v);
+        if (any && !(vtb::debug_flags() & 1024) && vtb::k9_seg_supported(a, w9, wgs, vtb::kSeg9Warm)) {
+            const size_t wsb = vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSeg9Warm);
             if (hipMalloc(&plan->seg9_ws, wsb) != hipSuccess) {
                 plan->seg9_ws = nullptr;
                 return VTB_ERR_NOMEM;
             }
             if (hipMemset(plan->seg9_ws, 0, 256) != hipSuccess) return VTB_ERR_DEVICE;  // the arrival counter
             plan->seg9_wgs = wgs;
+            plan->seg9_waves = w9;
         }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_out), plan->lat_out, 0) != hipSuccess ||
@@ -981,7 +984,7 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
             if (vtb::launch_k7_seg(a, plan->seg_waves, plan->seg_warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
         } else {
             a.ws = plan->seg9_ws;
-            if (vtb::launch_k9_seg(a, vtb::kSeg9Waves, plan->seg9_wgs, vtb::kSeg9Warm, d_done) != hipSuccess)
+            if (vtb::launch_k9_seg(a, plan->seg9_waves, plan->seg9_wgs, vtb::kSeg9Warm, d_done) != hipSuccess)
                 return VTB_ERR_DEVICE;
         }
         // wait on the completion word (the kernel's last write); a call that takes longer than

@@ -850,7 +850,7 @@ struct Seg9Args {
 };
 
 template <bool SOFT>
-__global__ __launch_bounds__(256) void k9_seg_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int T,
+__global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int T,
                                                      int L, int delta, int Tq, int dbg, Launch table,
                                                      uint8_t* __restrict__ ws, size_t ws_wave, Seg9Args a) {
     extern __shared__ uint4 smem4[];
@@ -1042,7 +1042,7 @@ size_t grid_waves(const Launch& a, int Tq) {
 // segment (multiple of 48) so that 2 W wgs segments cover Tq, G = the segments whose exact part
 // starts before Tq.
 bool k9_seg_geometry(int Tq, int W, int wgs, int warm, Seg9& sg, int& nwg) {
-    if (W < 1 || W > 4 || wgs < 1 || wgs > 64 || warm < kCh || warm % kCh) return false;
+    if (W < 1 || W > 8 || wgs < 1 || wgs > 64 || warm < kCh || warm % kCh) return false;
     const int G2 = 2 * W * wgs;
     int n = (Tq + (G2 - 1) * warm + G2 - 1) / G2;
     n = (n + kCh - 1) / kCh * kCh;
