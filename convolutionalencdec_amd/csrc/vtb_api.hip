@@ -53,6 +53,10 @@ struct vtb_plan {
     int seg_warm = 0;
     int seg9_wgs = 0;            // K = 9 SEG kernel workgroups (0: not usable for this plan)
     int seg9_waves = 0;          // and waves per workgroup
+    // adaptive SEG warm-up (vtb_decode_frame_sync): the short warm-up while frames converge
+    // with it; after a miss, the plan's warm-up for `seg_backoff` calls (doubling per miss)
+    bool seg_short = false;
+    int seg_backoff = 0, seg_skip = 0;
     void* seg9_ws = nullptr;     // its workspace (arrival counter, metrics, survivor words)
 };
 
@@ -356,6 +360,9 @@ long long vtb_debug_split_failures(vtb_plan_t* plan) {
 // Testing only (not in include/viterbi_amd.h): how vtb_decode_frame_sync calls ended, SEG
 // kernel decoded / SEG not converged (re-decoded) / no SEG kernel for the plan.
 static std::atomic<unsigned long long> g_seg_stats[3];
+// adaptive single-frame warm-up: after a miss of the short warm-up, the plan's own for 64 calls,
+// doubling per consecutive miss up to 4,096
+constexpr int kSegBackoff0 = 64, kSegBackoffMax = 4096;
 void vtb_debug_seg_stats(unsigned long long* out3) {
     for (int i = 0; i < 3; i++) out3[i] = g_seg_stats[i].load();
 }
@@ -939,12 +946,19 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         if (!wenv && !vtb::k7_seg_supported(a, waves, warm)) waves = 4;
         plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
+        const char* adapt = std::getenv("VTB_SEG_ADAPT");  // "0": the plan's warm-up only (measurement)
+        const bool short_ok = !std::getenv("VTB_SEG_WARM") && !(adapt && std::atoi(adapt) == 0);
+        plan->seg_short = short_ok && plan->seg_waves > 0 && vtb::k7_seg_supported(a, waves, vtb::kSegWarmShort);
+        plan->seg_backoff = kSegBackoff0;
         // K = 9: the frame over several workgroups ($VTB_SEG9_WGS: measurement)
         int wgs = vtb::kSeg9Wgs, w9 = vtb::kSeg9Waves;
         if (const char* v = std::getenv("VTB_SEG9_WGS")) wgs = std::atoi(v);
         if (const char* v = std::getenv("VTB_SEG9_WAVES")) w9 = std::atoi(v);
         if (any && !(vtb::debug_flags() & 1024) && vtb::k9_seg_supported(a, w9, wgs, vtb::kSeg9Warm)) {
-            const size_t wsb = vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSeg9Warm);
+            const bool s9 = short_ok && vtb::k9_seg_supported(a, w9, wgs, vtb::kSegWarmShort);
+            const size_t wsb = std::max(vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSeg9Warm),
+                                        s9 ? vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSegWarmShort) : size_t(0));
+            plan->seg_short = s9;
             if (hipMalloc(&plan->seg9_ws, wsb) != hipSuccess) {
                 plan->seg9_ws = nullptr;
                 return VTB_ERR_NOMEM;
@@ -964,7 +978,9 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
     std::memcpy(plan->lat_in, h_in, ib);
     volatile uint32_t* done = plan->lat_done;
     uint32_t status = 0;
-    if (plan->seg_waves > 0 || plan->seg9_wgs > 0) {
+    // one SEG launch at warm-up `warm`, waited for on the completion word: 1 decoded, 2 a
+    // segment boundary did not converge (nothing written), 0 with an error
+    auto run_seg = [&](int warm, int& st) -> int {
         *done = 0;
         std::atomic_thread_fence(std::memory_order_seq_cst);
         vtb::Launch a;
@@ -981,26 +997,51 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         a.cus = plan->cus;
         std::memcpy(a.symm, plan->symm, sizeof(a.symm));
         if (plan->seg_waves > 0) {
-            if (vtb::launch_k7_seg(a, plan->seg_waves, plan->seg_warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+            if (vtb::launch_k7_seg(a, plan->seg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
         } else {
             a.ws = plan->seg9_ws;
-            if (vtb::launch_k9_seg(a, plan->seg9_waves, plan->seg9_wgs, vtb::kSeg9Warm, d_done) != hipSuccess)
+            if (vtb::launch_k9_seg(a, plan->seg9_waves, plan->seg9_wgs, warm, d_done) != hipSuccess)
                 return VTB_ERR_DEVICE;
         }
         // wait on the completion word (the kernel's last write); a call that takes longer than
         // ~2 ms (first launch: code-object load) synchronises the stream instead
         const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t spin = 0; (status = *done) == 0; spin++) {
+        uint32_t v;
+        for (uint32_t spin = 0; (v = *done) == 0; spin++) {
             if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
                 if (hipStreamSynchronize(plan->stream) != hipSuccess) return VTB_ERR_DEVICE;
-                status = *done;
-                if (status == 0) return VTB_ERR_DEVICE;  // finished without reporting
+                v = *done;
+                if (v == 0) return VTB_ERR_DEVICE;  // finished without reporting
                 break;
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        st = int(v);
+        g_seg_stats[v == 1 ? 0 : 1]++;
+        return VTB_OK;
+    };
+    if (plan->seg_waves > 0 || plan->seg9_wgs > 0) {
+        const int wsafe = plan->seg_waves > 0 ? plan->seg_warm : vtb::kSeg9Warm;
+        int st = 0;
+        if (plan->seg_short && plan->seg_skip == 0) {
+            // the short warm-up first: any converged decode is exact, a miss costs one more launch
+            if (int r = run_seg(vtb::kSegWarmShort, st); r != VTB_OK) return r;
+            if (st == 1) {
+                plan->seg_backoff = kSegBackoff0;
+            } else {
+                plan->seg_skip = plan->seg_backoff;
+                plan->seg_backoff = std::min(2 * plan->seg_backoff, kSegBackoffMax);
+            }
+        } else {
+            if (plan->seg_skip > 0) plan->seg_skip--;
+        }
+        if (st != 1) {
+            if (int r = run_seg(wsafe, st); r != VTB_OK) return r;
+        }
+        status = uint32_t(st);
+    } else {
+        g_seg_stats[2]++;
     }
-    g_seg_stats[status == 1 ? 0 : status == 2 ? 1 : 2]++;
     if (status != 1) {
         // not converged (status 2) or no SEG kernel for this plan: the frame kernel, input from
         // the same host-mapped buffer through one copy, output written straight to host memory

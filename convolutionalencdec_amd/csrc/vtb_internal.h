@@ -123,6 +123,7 @@ hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s);
 // of `waves` waves, input staged through LDS, survivors and metrics in a workspace (whose
 // first word, an arrival counter, must be zero before the first launch), *done as for K=7.
 constexpr int kSeg9Waves = 4, kSeg9Wgs = 4, kSeg9Warm = 96;
+constexpr int kSegWarmShort = 48;  // single-frame paths: the short warm-up tried first
 bool k9_seg_supported(const Launch& a, int waves, int wgs, int warm);
 size_t k9_seg_workspace_bytes(const Launch& a, int waves, int wgs, int warm);
 hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t* done);

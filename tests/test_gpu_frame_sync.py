@@ -159,6 +159,37 @@ def test_k9_pure_noise_falls_back(orc, monkeypatch):
     assert seg_stats()[1] > s0[1]
 
 
+@pytest.mark.parametrize("K", [7, 9])
+def test_adaptive_warmup(orc, K, monkeypatch):
+    """The short warm-up (48 steps) is tried first; after a miss the plan's own warm-up serves
+    the next 64 calls (doubling per miss), so a noisy stretch costs one extra launch per
+    backoff period, and clean frames take one launch each.  Bit-exact throughout."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    monkeypatch.delenv("VTB_SEG_WARM", raising=False)
+    monkeypatch.delenv("VTB_SEG_ADAPT", raising=False)
+    L = 2048
+    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
+    unc, clean = random_frames(orc, K, L, 12, 0.0, seed=31 + K)
+    s0 = seg_stats()
+    assert (run(d, clean) == orc.decode(K, CODES[K], clean, L)).all()
+    s1 = seg_stats()
+    assert (s1 - s0).tolist() == [12, 0, 0], (s0, s1)  # one converged launch per clean frame
+    unc, noise = random_frames(orc, K, L, 20, 0.5, seed=37 + K)
+    assert (run(d, noise) == orc.decode(K, CODES[K], noise, L)).all()
+    s2 = seg_stats()
+    assert s2[1] - s1[1] <= 20 + 1, (s1, s2)  # one short-warm-up miss, then the plan's warm-up only
+    assert s2[2] == s1[2]
+
+
+def test_adaptive_off(orc, monkeypatch):
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    monkeypatch.setenv("VTB_SEG_ADAPT", "0")
+    L = 3000
+    unc, rx = random_frames(orc, 7, L, 6, 0.03, seed=3)
+    d = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L)
+    assert (run(d, rx) == orc.decode(7, CODES[7], rx, L)).all()
+
+
 def test_short_frames(orc, monkeypatch):
     monkeypatch.delenv("VTB_KERNEL", raising=False)
     for L in (1, 8, 100, 233):
