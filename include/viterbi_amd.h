@@ -155,12 +155,13 @@ int vtb_decode_peer_multi(const vtb_code_t* code, vtb_input_t input, int32_t fra
  * single-frame form of vtb_decode_host for callers that decode frame by frame (the legacy
  * VITERBI_DECODER_HARD contract, one frame per call).  h_in holds one frame in the plan's
  * input layout, h_out receives ceil(L/8) bytes.  K = 7 frames (T >= 240) are cut into up to
- * eight segments decoded at once by the waves of one workgroup (each segment after the first
- * starts 96 steps early from equal metrics and is used once its metrics provably match its
- * predecessor's; otherwise the frame is decoded whole), reading the frame from and writing
- * the bytes to plan-owned host-mapped memory, with completion signalled through host memory
- * instead of a stream synchronisation.  Bit-exact with vtb_decode_host.  The plan's stream and
- * buffers are used: one host thread per plan at a time. */
+ * 16 segments decoded at once by the waves of one workgroup, K = 9 frames into up to 32 over
+ * four workgroups (each segment after the first starts 48 or 96 steps early from equal metrics
+ * and is used once its metrics provably match its predecessor's; otherwise the frame is decoded
+ * again with the longer warm-up, then whole), reading the frame from and writing the bytes to
+ * plan-owned host-mapped memory, with completion signalled through host memory instead of a
+ * stream synchronisation.  Bit-exact with vtb_decode_host.  The plan's stream, buffers and
+ * warm-up state are used: one host thread per plan at a time. */
 int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out);
 
 /* One hard-input frame of `segments` coded segments from host memory (the legacy
