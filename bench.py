@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="measure the streaming decoder (vtb_stream_*, SURVEY.md 8 f3) instead: every stream "
                          "receives this many segments per step, one long frame per stream")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group for the timing barrier and max-reduction (nccl = RCCL; gloo: rehearsal)")
     ap.add_argument("--gen", choices=("host", "device"), default="host",
                     help="synthetic frames from numpy on the host (default) or from the device generator "
                          "(csrc/vtb_gen.hip: no PCIe, for large batches)")
@@ -279,8 +281,12 @@ def main():
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # VTB_BENCH_ONE_DEVICE=1 (rehearsal of the N > 1 path on a one-GPU box, with
+    # --dist-backend gloo): every rank on device 0
+    gpu = 0 if os.environ.get("VTB_BENCH_ONE_DEVICE") == "1" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    local = gpu
     if args.stream_chunk > 0:
         if world > 1:
             raise SystemExit("--stream-chunk is a single-GPU measurement")
@@ -288,13 +294,17 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
         def barrier():
             dist.barrier()
 
         def allreduce_max(x):
-            t = torch.tensor([x], dtype=torch.float64, device=dev)
+            t = torch.tensor([x], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item())
     else:
