@@ -39,6 +39,45 @@ static vtb_genk_code_t legacy_genk_code(void) {
     return c;
 }
 
+/* The reference library draws nothing from rand(); the GPU runtime does (libhsa-runtime64
+ * imports rand and srand).  Harnesses such as berTestK7.c build their channel from rand()
+ * between decoder calls (berTestK7.c:29-43, 135-138), so every call into the GPU keeps the
+ * caller's rand() stream: glibc's random state (the state array and its position word) is
+ * copied before the call and put back after it, through initstate / setstate only.
+ * initstate / setstate return and take the address of a state's position word, which is
+ * followed by the state array (glibc random.c); the state's type is that word mod 5. */
+typedef struct {
+    int32_t* pos;      /* the caller's position word */
+    int words;         /* position word + state array */
+    int32_t saved[64]; /* their contents before the call */
+} rand_keep_t;
+static __thread int32_t rand_scratch[32]; /* a TYPE_3 state of our own (128 bytes) */
+
+static void rand_keep_begin(rand_keep_t* kp) {
+    static const int deg[5] = {0, 7, 15, 31, 63};
+    char* cur = initstate(1u, (char*)rand_scratch, sizeof(rand_scratch)); /* stores the caller's position */
+    kp->pos = (int32_t*)cur;
+    const int d = deg[kp->pos[0] % 5];
+    kp->words = 1 + (d > 0 ? d : 1);
+    memcpy(kp->saved, kp->pos, (size_t)kp->words * sizeof(int32_t));
+    setstate(cur); /* back to the caller's state, unchanged */
+}
+
+static void rand_keep_end(rand_keep_t* kp) {
+    setstate((char*)rand_scratch); /* leave the caller's state (its position word is rewritten) */
+    memcpy(kp->pos, kp->saved, (size_t)kp->words * sizeof(int32_t));
+    setstate((char*)kp->pos); /* and return to it as it was before the call */
+}
+
+#define KEEP_RAND(call)            \
+    ({                             \
+        rand_keep_t kr_;           \
+        rand_keep_begin(&kr_);     \
+        int kr_r = (call);         \
+        rand_keep_end(&kr_);       \
+        kr_r;                      \
+    })
+
 static void gpu_failed(const char* what, int r) {
     printf("viterbi: GPU %s failed: %s (%d)\n", what, vtb_strerror(r), r);
     exit(1);
@@ -161,7 +200,7 @@ static int decode_staged(viterbiHardState_t* VTB_LEGACY_RESTRICT state, const ui
         return 0;
     }
     vtb_code_t c = legacy_code();
-    int r = vtb_decode_frame_legacy(&c, frame, segments, uncoded);
+    int r = KEEP_RAND(vtb_decode_frame_legacy(&c, frame, segments, uncoded));
     if (r < 0) gpu_failed("decode", r);
     return r;
 }
@@ -182,7 +221,7 @@ int viterbiDecoderHardButterflyk1(viterbiHardState_t* VTB_LEGACY_RESTRICT state,
             /* the reference's uint8 metric update and renormalisation phase (:101-191) */
             vtb_code_t c = legacy_code();
             uint32_t counter = state->renormCounter;
-            int r = vtb_legacy_metrics_k1(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter);
+            int r = KEEP_RAND(vtb_legacy_metrics_k1(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter));
             if (r != VTB_OK) gpu_failed("metric update", r);
             state->renormCounter = counter;
         }
@@ -225,7 +264,7 @@ int viterbiDecoderHard(viterbiHardState_t* VTB_LEGACY_RESTRICT state, uint8_t* V
              * ones a step before */
             uint32_t m[NUM_STATES], prev[NUM_STATES];
             for (unsigned s = 0; s < NUM_STATES; s++) m[s] = (uint32_t)(*state->nodeMetricsCur)[s];
-            int r = vtb_legacy_metrics_genk(&c, codedSegments, segmentsIn, m, prev);
+            int r = KEEP_RAND(vtb_legacy_metrics_genk(&c, codedSegments, segmentsIn, m, prev));
             if (r != VTB_OK) gpu_failed("metric update", r);
             if (segmentsIn & 1) swapViterbiArrays(state);
             for (unsigned s = 0; s < NUM_STATES; s++) {
@@ -248,7 +287,7 @@ int viterbiDecoderHard(viterbiHardState_t* VTB_LEGACY_RESTRICT state, uint8_t* V
         printf("viterbi: frame of %d segments does not hold a whole number of bytes after the %d tail segments; "
                "nothing decoded\n", segments, S);
     } else {
-        r = vtb_genk_decode_frame_legacy(&c, frame, segments, uncoded);
+        r = KEEP_RAND(vtb_genk_decode_frame_legacy(&c, frame, segments, uncoded));
         if (r < 0) gpu_failed("decode", r);
     }
     resetViterbiDecoderHard(state);

@@ -179,3 +179,70 @@ def test_metrics_k1_random_chunkings_vs_oracle(orc, K, g):
             assert (m == want).all(), (K, g, f, pos)
             pos += n
             assert counter == _renorm_phase(pos)
+
+
+def _reference_program(name, timeout):
+    """A reference test program built unchanged against the drop-in (oracle/Makefile
+    `harness`: make -C oracle harness, in the build container; the binary travels with the
+    tree).  Returns (exit status, stdout)."""
+    import subprocess
+
+    from helpers import REPO
+
+    exe = os.path.join(REPO, "oracle", "_ref", name)
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (make -C oracle harness where the reference sources are)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    return r.returncode, r.stdout + r.stderr
+
+
+def test_reference_handtraced_program_on_gpu():
+    """handTracedTest/handTraced.c, unchanged, with its K=3 test code (0b111, 0b110): its
+    encoder known answer passes (its own asserts), then viterbiConfigCheck stops it with exit
+    status 1, as the reference's own check does for this code (viterbiDecoder.c:15-26 under
+    USE_POLY_SYMMETRY, which viterbiDecoder.h:39 defines): the drop-in keeps the reference's
+    error behaviour.  The program's decoder known answers are checked below through the
+    drop-in's entry points."""
+    rc, out = _reference_program("handTraced_amd", 120)
+    assert rc == 1, out[-2000:]
+    assert "Encoded: 0x68, Got 10 coded segments" in out
+    assert "Polynomial 1 does not depend on the input bit and the last bit, therefore polynomial symmetry cannot be used" in out
+
+
+def test_handtraced_node_metric_known_answers():
+    """handTraced.c:70-111's hand-traced node metrics after each of four one-segment
+    last=false calls on its corrupted frame: the reference's own known answers, literally,
+    through the drop-in's generic-trellis metric update (vtb_legacy_metrics_genk with k = 1,
+    the update of viterbiDecoderHard, viterbiDecoder.c:84-131, which handTraced's Makefile
+    builds).  The butterfly update (vtb_legacy_metrics_k1, like viterbiDecoderButterflyk1.c)
+    assumes generator symmetry this code lacks (the reason viterbiConfigCheck refuses it) and
+    differs from the hand trace at state 3 after the first segment (6, not 5); the random
+    chunkings test above pins that form to the oracle."""
+    from convolutionalencdec_amd import native
+
+    g = (0b111, 0b110)
+    code = native.VtbGenKCode.make(1, 3, g)
+    corrupted = np.array([0b01, 0b11, 0b01, 0b10, 0b10, 0b11, 0b01, 0, 0, 0], np.uint8)
+    m = np.array([0, 5, 5, 5], np.uint32)  # after VITERBI_RESET (handTraced.c:72-75)
+    want = [[1, 1, 6, 5], [3, 1, 1, 3], [1, 3, 2, 2], [2, 2, 2, 4]]  # [0], [1], [2], [3]
+    for i in range(4):
+        seg = np.ascontiguousarray(corrupted[i:i + 1])
+        assert native.lib().vtb_legacy_metrics_genk(ctypes.byref(code), vp(seg), 1, vp(m), None) == 0
+        assert m.tolist() == want[i], (i, m.tolist())
+    k1, _ = _metrics_k1(3, g, corrupted[:1], np.array([0, 5, 5, 5], np.uint8), 0)
+    assert k1.tolist() == [1, 1, 6, 6]
+
+
+def test_reference_bertestk7_program_on_gpu():
+    """berTestK7/berTestK7.c, unchanged: 3 x 10,000 2,048-bit frames (glibc rand() channel at
+    the three BSC points) decoded one frame per call through the drop-in on the GPU; its own
+    pass criterion, and the decoded bit errors equal to the reference's run (92418 / 9655 /
+    655)."""
+    from helpers import BERTEST_ERRORS
+
+    rc, out = _reference_program("berTestK7_amd", 300)
+    assert rc == 0, out[-2000:]
+    assert "Success!" in out, out[-2000:]
+    rows = [ln.split("|") for ln in out.splitlines() if ln.count("|") == 2 and ln.strip()[:1] in "-0123456789"]
+    decoded_errors = tuple(int(r[2].split()[2]) for r in rows)
+    assert decoded_errors == BERTEST_ERRORS, (decoded_errors, out[-2000:])
