@@ -120,6 +120,35 @@ def test_legacy_encoder_streams_across_calls():
     assert (out == rx[0]).all()
 
 
+@pytest.mark.parametrize("K", [5, 7, 9])
+def test_legacy_encoder_random_splits_vs_oracle(K):
+    """The drop-in encoder's byte-table path (k = 1, csrc/legacy/convEncode.c) on random
+    payloads split over random last=false calls, against the oracle's bit-serial encoder."""
+    from helpers import Oracle
+
+    orc = Oracle()
+    lib = _legacy(K)
+    enc = (ctypes.c_uint8 * 64)()
+    rng = np.random.default_rng(K)
+    for trial in range(20):
+        nb = int(rng.integers(1, 600))
+        row = rng.integers(0, 256, nb, dtype=np.uint8)
+        want = orc.encode(K, CODES[K], row[None, :])[0]
+        out = np.zeros(want.size + 16, np.uint8)
+        lib.resetConvEncoder(enc)
+        lib.initConvEncoder(enc)
+        cuts = sorted(set(int(c) for c in rng.integers(0, nb, int(rng.integers(0, 5))))) + [nb]
+        start, written = 0, 0
+        for cut in cuts:
+            seg = np.ascontiguousarray(row[start:cut])
+            dst = out[written:]
+            written += lib.convEnc(enc, seg.ctypes.data_as(ctypes.c_void_p), dst.ctypes.data_as(ctypes.c_void_p),
+                                   len(seg), cut == nb)
+            start = cut
+        assert written == want.size and (out[:written] == want).all(), (K, trial, nb, cuts)
+        assert (out[written:] == 0).all()
+
+
 def test_calc_hamming_dist():
     lib = _legacy(7)
     assert lib.calcHammingDist(0b11, 0b00, 2) == 2
