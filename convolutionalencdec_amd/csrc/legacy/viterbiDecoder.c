@@ -52,10 +52,15 @@ typedef struct {
     int32_t saved[64]; /* their contents before the call */
 } rand_keep_t;
 static __thread int32_t rand_scratch[32]; /* a TYPE_3 state of our own (128 bytes) */
+static __thread int rand_scratch_ready;
 
 static void rand_keep_begin(rand_keep_t* kp) {
     static const int deg[5] = {0, 7, 15, 31, 63};
-    char* cur = initstate(1u, (char*)rand_scratch, sizeof(rand_scratch)); /* stores the caller's position */
+    if (!rand_scratch_ready) { /* seed the scratch state once per thread (initstate runs 310 draws) */
+        setstate(initstate(1u, (char*)rand_scratch, sizeof(rand_scratch)));
+        rand_scratch_ready = 1;
+    }
+    char* cur = setstate((char*)rand_scratch); /* stores the caller's position in its state */
     kp->pos = (int32_t*)cur;
     const int d = deg[kp->pos[0] % 5];
     kp->words = 1 + (d > 0 ? d : 1);
