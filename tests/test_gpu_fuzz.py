@@ -30,7 +30,12 @@ def gpu_present():
         pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
 
 
-def _cases(n=128, seed=20261016):
+# VTB_FUZZ_N / VTB_FUZZ_SEED: a longer sweep on demand (the default is the committed sweep)
+FUZZ_N = int(os.environ.get("VTB_FUZZ_N", "0"))
+FUZZ_SEED = int(os.environ.get("VTB_FUZZ_SEED", "0"))
+
+
+def _cases(n=FUZZ_N or 128, seed=FUZZ_SEED or 20261016):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
@@ -80,7 +85,7 @@ def test_random_case_vs_oracle(orc, case):
     assert bad.size == 0, (case, bad.size, bad[:8])
 
 
-def _frame_cases(n=72, seed=20261017):
+def _frame_cases(n=FUZZ_N or 72, seed=(FUZZ_SEED + 1) if FUZZ_SEED else 20261017):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
