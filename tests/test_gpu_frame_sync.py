@@ -208,3 +208,46 @@ def test_repeated_calls_one_plan(orc, monkeypatch):
     for rep in range(3):
         for i in range(16):
             assert (d.decode_frame(rx[i]) == want[i]).all(), (rep, i)
+
+
+@pytest.mark.parametrize("nthreads", [4, 12])
+def test_concurrent_threads(orc, nthreads, monkeypatch):
+    """Host threads decoding at once (one plan each, as the legacy API's per-thread plans):
+    mixed shapes (two frame lengths, soft and hard, K=9) side by side, every frame
+    bit-exact."""
+    import threading
+
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    shapes = [(7, 2048, False), (7, 2048, False), (7, 1000, True), (9, 2048, False)]
+    jobs = []
+    for i in range(nthreads):
+        K, L, soft = shapes[i % len(shapes)]
+        if soft:
+            unc, rx = random_frames(orc, K, L, 24, 0.0, seed=700 + i, soft=True, sigma=0.5)
+        else:
+            unc, rx = random_frames(orc, K, L, 24, 0.02 if i % 3 else 0.0, seed=700 + i)
+        jobs.append((K, L, soft, rx, orc.decode(K, CODES[K], rx, L, soft=soft)))
+    decs = [ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft) for K, L, soft, _, _ in jobs]
+    for d, (K, L, soft, rx, want) in zip(decs, jobs):
+        d.decode_frame(rx[0])  # plans and host-mapped buffers before the threads start
+    errors = []
+
+    def work(i):
+        K, L, soft, rx, want = jobs[i]
+        try:
+            for rep in range(3):
+                for f in range(rx.shape[0]):
+                    got = decs[i].decode_frame(rx[f])
+                    if not (got == want[f]).all():
+                        errors.append((i, rep, f))
+                        return
+        except Exception as e:  # noqa: BLE001
+            errors.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors[:8]
