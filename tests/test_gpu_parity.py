@@ -25,10 +25,19 @@ KERNELS = ("auto", "k7", "gws", "k7s", "k9", "lds")
 
 class Kern(str):
     def need(self, K):
-        if self in ("k7", "gws", "k7s") and K != 7:
-            pytest.skip(f"kernel {self} is K=7 only")
-        if self == "k9" and K != 9:
-            pytest.skip("kernel k9 is K=9 only")
+        assert K in KS_OF.get(str(self), (K,)), (self, K)  # (combinations are generated valid)
+
+
+KS_OF = {"k7": (7,), "gws": (7,), "k7s": (7,), "k9": (9,)}  # kernel families tied to one K
+
+
+def kernels_for(K):
+    return [k for k in KERNELS if K in KS_OF.get(k, (K,))]
+
+
+def kk(Ks):
+    """(K, kernel) pairs: every kernel family that decodes K."""
+    return [(K, k) for K in Ks for k in kernels_for(K)]
 
 
 @pytest.fixture(scope="module")
@@ -42,7 +51,7 @@ def gpu_present():
         pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
 
 
-@pytest.fixture(params=KERNELS)
+@pytest.fixture
 def kernel(request, monkeypatch):
     if request.param == "auto":
         monkeypatch.delenv("VTB_KERNEL", raising=False)
@@ -58,7 +67,7 @@ def dev_decode(dec, frames):
     return out.cpu().numpy()
 
 
-@pytest.mark.parametrize("K", [5, 7, 9])
+@pytest.mark.parametrize("K,kernel", kk([5, 7, 9]), indirect=["kernel"])
 def test_hard_golden_vectors(K, kernel):
     kernel.need(K)
     for key, L, unc, rx, dec in golden_sets(K):
@@ -67,7 +76,7 @@ def test_hard_golden_vectors(K, kernel):
         assert (dev_decode(d, rx) == dec).all(), (K, key)
 
 
-@pytest.mark.parametrize("K", [5, 7, 9])
+@pytest.mark.parametrize("K,kernel", kk([5, 7, 9]), indirect=["kernel"])
 def test_soft_bridge_golden_vectors(K, kernel):
     """Soft input q = 255*bit must reproduce the reference's hard decode bit for bit."""
     kernel.need(K)
@@ -76,7 +85,9 @@ def test_soft_bridge_golden_vectors(K, kernel):
         assert (dev_decode(d, hard_to_soft(rx)) == dec).all(), (K, key)
 
 
-@pytest.mark.parametrize("K,g", [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]), (9, CODES[9])])
+@pytest.mark.parametrize("K,g,kernel", [(K, g, k) for K, g in [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]),
+                                                              (9, CODES[9])] for k in kernels_for(K)],
+                         indirect=["kernel"])
 @pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000])
 def test_hard_random_vs_oracle(orc, K, g, L, kernel):
     kernel.need(K)
@@ -91,7 +102,7 @@ def test_hard_random_vs_oracle(orc, K, g, L, kernel):
             assert (got == unc).all()
 
 
-@pytest.mark.parametrize("K", [5, 7, 9])
+@pytest.mark.parametrize("K,kernel", kk([5, 7, 9]), indirect=["kernel"])
 @pytest.mark.parametrize("L", [9, 1024, 2048])
 def test_soft_random_vs_oracle(orc, K, L, kernel):
     kernel.need(K)
@@ -123,7 +134,9 @@ def test_split_frames_vs_oracle(orc, L, soft):
 
 
 @pytest.mark.parametrize("soft", [False, True])
-@pytest.mark.parametrize("K,L,F", [(7, 1024, 12289), (7, 1024, 40961), (9, 512, 20481)])
+@pytest.mark.parametrize("K,L,F,kernel", [(K, L, F, k) for K, L, F in [(7, 1024, 12289), (7, 1024, 40961), (9, 512, 20481)]
+                                          for k in kernels_for(K) if k != "lds" and not (k == "k7" and F > 20000)],
+                         indirect=["kernel"])
 def test_persistent_grid_many_pairs_per_wave(orc, K, L, F, soft, kernel):
     """Batches with several frame pairs per wave of the persistent grid (more pairs than the
     CUs hold at once), an odd frame count (the last pair has one frame), the next pair's
@@ -131,8 +144,6 @@ def test_persistent_grid_many_pairs_per_wave(orc, K, L, F, soft, kernel):
     from convolutionalencdec_amd import frames as devframes
 
     kernel.need(K)
-    if kernel == "lds" or (kernel == "k7" and F > 20000):
-        pytest.skip("covered at smaller sizes for this kernel family")
     code = ConvCode(K, CODES[K])
     unc, rx = devframes.make_frames(code, F, L, soft=soft, snr_db=-4.0, p=0.04, seed=F + K)
     d = ViterbiDecoder(code, frame_bits=L, soft=soft)
@@ -144,13 +155,14 @@ def test_persistent_grid_many_pairs_per_wave(orc, K, L, F, soft, kernel):
 
 @pytest.mark.parametrize("soft", [False, True])
 @pytest.mark.parametrize("L", [10000, 16384])
+@pytest.mark.parametrize("kernel", [k for k in kernels_for(7) if k != "k7"], indirect=True)
 def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
     """Frames past the LDS-resident kernel's survivor capacity up to the API maximum
     (VTB_MAX_FRAME_BITS, reference viterbiDecoder.h:18): the global-survivor variant."""
     K = 7
     kernel.need(K)
-    if kernel == "k7" or (kernel == "lds" and soft and L == 16384):
-        pytest.skip("survivors of this frame length exceed one CU's LDS for this kernel family")
+    if kernel == "lds" and soft and L == 16384:
+        pytest.skip("survivors of this frame length exceed one CU's LDS for the generic kernel")
     if soft:
         unc, x = random_frames(orc, K, L, 67, 0.0, 31 + L, soft=True, sigma=0.6287)
     else:
@@ -161,6 +173,7 @@ def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
 
 @pytest.mark.parametrize("soft", [False, True])
 @pytest.mark.parametrize("L", [4095, 16384])
+@pytest.mark.parametrize("kernel", kernels_for(9), indirect=True)
 def test_k9_long_frames_vs_oracle(orc, L, soft, kernel):
     """K=9 frames up to the API maximum (reference viterbiDecoder.h:18), odd and even T."""
     K = 9
@@ -175,7 +188,7 @@ def test_k9_long_frames_vs_oracle(orc, L, soft, kernel):
     assert (dev_decode(d, x) == orc.decode(K, CODES[K], x, L, soft=soft)).all()
 
 
-@pytest.mark.parametrize("K", [7, 9])
+@pytest.mark.parametrize("K,kernel", kk([7, 9]), indirect=["kernel"])
 def test_soft_extreme_values(orc, K, kernel):
     """Saturated, constant and alternating soft inputs (tie-heavy) match the oracle."""
     kernel.need(K)
@@ -189,6 +202,7 @@ def test_soft_extreme_values(orc, K, kernel):
         assert (dev_decode(d, q) == orc.decode(K, CODES[K], q, L, soft=True)).all()
 
 
+@pytest.mark.parametrize("kernel", kernels_for(7), indirect=True)
 def test_bertest_k7_kat_on_gpu(orc, kernel):
     """The reference berTestK7 stream (glibc rand seed 9865, 3 x 10000 packets) decoded on
     the GPU gives exactly the reference's decoded bit-error counts."""
@@ -227,6 +241,7 @@ def test_full_size_soft_batch_properties(orc):
 
 
 @pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("kernel", kernels_for(9), indirect=True)
 def test_k9_full_config(orc, kernel, soft):
     """C4: K=9, 4096 x 1024 -- every frame against the oracle (hard at BSC p = 0.03, soft at
     the bench's SNR), and the decoded BER."""
