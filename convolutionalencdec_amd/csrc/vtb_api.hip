@@ -906,6 +906,21 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
     return VTB_OK;
 }
 
+// A failed first call leaves no half-built single-frame state: the next call starts over.
+static int lat_undo(vtb_plan_t* plan, int err) {
+    if (plan->seg9_ws) (void)hipFree(plan->seg9_ws);
+    if (plan->lat_in) (void)hipHostFree(plan->lat_in);
+    if (plan->lat_out) (void)hipHostFree(plan->lat_out);
+    if (plan->lat_done) (void)hipHostFree(plan->lat_done);
+    plan->seg9_ws = nullptr;
+    plan->seg9_wgs = plan->seg9_waves = 0;
+    plan->lat_in = plan->lat_out = nullptr;
+    plan->lat_done = nullptr;
+    plan->lat_d_in = plan->lat_d_out = nullptr;
+    plan->lat_d_done = nullptr;
+    return err;
+}
+
 int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out) {
     if (!plan || !h_in || !h_out) return VTB_ERR_INVALID;
     DeviceGuard g(plan->device);
@@ -961,16 +976,16 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
             plan->seg_short = s9;
             if (hipMalloc(&plan->seg9_ws, wsb) != hipSuccess) {
                 plan->seg9_ws = nullptr;
-                return VTB_ERR_NOMEM;
+                return lat_undo(plan, VTB_ERR_NOMEM);
             }
-            if (hipMemset(plan->seg9_ws, 0, 256) != hipSuccess) return VTB_ERR_DEVICE;  // the arrival counter
+            if (hipMemset(plan->seg9_ws, 0, 256) != hipSuccess) return lat_undo(plan, VTB_ERR_DEVICE);  // arrival counter
             plan->seg9_wgs = wgs;
             plan->seg9_waves = w9;
         }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_out), plan->lat_out, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_done), plan->lat_done, 0) != hipSuccess)
-            return VTB_ERR_DEVICE;
+            return lat_undo(plan, VTB_ERR_DEVICE);
     }
     uint8_t *d_in = plan->lat_d_in, *d_out = plan->lat_d_out;
     uint32_t* d_done = plan->lat_d_done;
