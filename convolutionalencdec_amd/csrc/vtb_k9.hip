@@ -63,8 +63,12 @@ using k7::uniform64;
 constexpr int kCh = 48;                  // ACS steps per unrolled chunk (multiple of 8 and 16)
 constexpr int kCol = 49;                 // 8-byte slots per table column (48 rows + bank skew)
 constexpr int kRingBytes = 8 * kCol * 8;  // branch-metric ring: 8 (label, R) columns
-constexpr int kAH = 2;                   // table rows read this many steps ahead
-constexpr int kRS = 3;                   // register ring slots (48 % kRS == 0)
+#ifndef VTB_EXP_K9AH
+#define VTB_EXP_K9AH 2
+#define VTB_EXP_K9RS 3
+#endif
+constexpr int kAH = VTB_EXP_K9AH;        // table rows read this many steps ahead
+constexpr int kRS = VTB_EXP_K9RS;        // register ring slots (48 % kRS == 0)
 constexpr int kTbWarm = 48;              // traceback warm-up steps past a block's end
 constexpr uint32_t kR1 = 0x10001u;
 constexpr int kColBytes = 1024;          // survivor column: 256 words per 16 steps

@@ -24,6 +24,8 @@ for v in "$@"; do
     warm144) build warm144 -DVTB_EXP_TBWARM=144 ;;
     noword) build noword -DVTB_EXP_NO_WORD ;;
     base) build base ;;
+    k9ah3) build k9ah3 -DVTB_EXP_K9AH=3 -DVTB_EXP_K9RS=4 ;;
+    k9ah5) build k9ah5 -DVTB_EXP_K9AH=5 -DVTB_EXP_K9RS=6 ;;
     noprio) build noprio -DVTB_EXP_NOPRIO ;;
     tbspec) build tbspec -DVTB_EXP_TBSPEC ;;
     nonop) build nonop -DVTB_EXP_NONOP ;;
