@@ -1215,7 +1215,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // CUs hold in one round and for the streaming decoder (the loop's extra live state costs
 // ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
 template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false, bool LIST = false>
-__global__ __launch_bounds__(64) void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+#ifdef VTB_EXP_WPE
+#define VTB_K7_WPE __attribute__((amdgpu_waves_per_eu(1, VTB_EXP_WPE)))
+#else
+#define VTB_K7_WPE
+#endif
+__global__ __launch_bounds__(64) VTB_K7_WPE void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
                                                     uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa) {

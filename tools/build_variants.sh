@@ -25,6 +25,8 @@ for v in "$@"; do
     noword) build noword -DVTB_EXP_NO_WORD ;;
     base) build base ;;
     k9ah3) build k9ah3 -DVTB_EXP_K9AH=3 -DVTB_EXP_K9RS=4 ;;
+    wpe2) build wpe2 -DVTB_EXP_WPE=2 ;;
+    wpe4) build wpe4 -DVTB_EXP_WPE=4 ;;
     k9ah5) build k9ah5 -DVTB_EXP_K9AH=5 -DVTB_EXP_K9RS=6 ;;
     noprio) build noprio -DVTB_EXP_NOPRIO ;;
     tbspec) build tbspec -DVTB_EXP_TBSPEC ;;
