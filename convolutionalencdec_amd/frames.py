@@ -18,6 +18,16 @@ def _stream(t, stream):
     return stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _check_rows(t, min_cols, what):
+    """A [rows, >= min_cols] torch.uint8 tensor on a ROCm device (the kernels read whole rows)."""
+    import torch
+
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or t.device.type != "cuda" or t.dim() != 2:
+        raise TypeError(f"{what} must be a 2-D torch.uint8 tensor on a ROCm device")
+    if t.shape[1] < min_cols:
+        raise ValueError(f"{what} rows hold {t.shape[1]} bytes, {min_cols} needed")
+
+
 def payload(frames, frame_bits, seed, device=0, stream=None):
     """[frames, ceil(L/8)] uint8 payload rows (MSB-first bits) on cuda:`device`."""
     import torch
@@ -39,6 +49,7 @@ def encode(code, frame_bits, unc, stream=None):
 
     code = code if isinstance(code, ConvCode) else ConvCode(*code)
     T = int(frame_bits) + code.S
+    _check_rows(unc, (int(frame_bits) + 7) // 8, "encode: unc")
     out = torch.empty((unc.shape[0], T), dtype=torch.uint8, device=unc.device)
     c = code._c()
     if unc.stride(1) != 1:
@@ -56,6 +67,7 @@ def channel(coded, soft, param, seed, stream=None):
     SNR dB) -> [F, T, 2] bytes."""
     import torch
 
+    _check_rows(coded, 1, "channel: coded")
     F, T = coded.shape
     if coded.stride(1) != 1:
         coded = coded.contiguous()

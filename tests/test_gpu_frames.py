@@ -79,3 +79,11 @@ def test_end_to_end(orc, soft):
     assert (out == ref).all()
     unc2, rx2 = frames.make_frames(code, F, L, soft=soft, snr_db=10.0, p=0.0, seed=22)
     assert (dec.decode_device(rx2.reshape(F, -1)).cpu().numpy() == unc2.cpu().numpy()).all()
+
+
+def test_encode_rejects_short_rows():
+    import torch
+
+    unc = torch.zeros((4, 127), dtype=torch.uint8, device="cuda:0")  # 1024 bits need 128 bytes
+    with pytest.raises(ValueError):
+        frames.encode(ConvCode(), 1024, unc)
