@@ -216,6 +216,8 @@ class ViterbiStream:
         else:
             if chunk.dtype != torch.uint8 or not chunk.is_cuda:
                 raise TypeError("push expects a torch.uint8 tensor on a ROCm device")
+            if chunk.device.index != self.device:
+                raise ValueError(f"chunk is on {chunk.device}, the streams on cuda:{self.device}")
             x = chunk.reshape(self.streams, -1)
             if x.stride(1) != 1:
                 x = x.contiguous()
