@@ -203,18 +203,24 @@ int run_forward(const FwdArgs& a, const uint8_t* segments, uint32_t* met_io, uin
     if (r != VTB_OK) return r;
     const size_t mb = size_t(a.N) * sizeof(uint32_t);
     uint32_t* d_cnt = c.d_met + 2 * 256;
+    uint32_t tmp[512];
+    // every error exit after the first asynchronous copy drains the stream first: queued copies
+    // still read the caller's buffers and write tmp (this frame)
+    auto fail = [&]() {
+        (void)hipStreamSynchronize(c.stream);
+        return VTB_ERR_DEVICE;
+    };
     if (hipMemcpyAsync(c.d_seg, segments, size_t(a.count), hipMemcpyHostToDevice, c.stream) != hipSuccess ||
         hipMemcpyAsync(c.d_met, met_io, mb, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
         (counter && hipMemcpyAsync(d_cnt, counter, sizeof(uint32_t), hipMemcpyHostToDevice, c.stream) != hipSuccess))
-        return VTB_ERR_DEVICE;
+        return fail();
     const int threads = a.N < 64 ? 64 : a.N;
     hipLaunchKernelGGL(legacy_forward_kernel, dim3(1), dim3(threads), 0, c.stream, c.d_seg, c.d_met, d_cnt, a);
-    if (hipGetLastError() != hipSuccess) return VTB_ERR_DEVICE;
-    uint32_t tmp[512];
+    if (hipGetLastError() != hipSuccess) return fail();
     if (hipMemcpyAsync(tmp, c.d_met, 2 * mb, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
         (counter && hipMemcpyAsync(counter, d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream) != hipSuccess) ||
         hipStreamSynchronize(c.stream) != hipSuccess)
-        return VTB_ERR_DEVICE;
+        return fail();
     std::memcpy(met_io, tmp, mb);
     if (prev) std::memcpy(prev, tmp + a.N, mb);
     return VTB_OK;
@@ -268,16 +274,20 @@ int vtb_genk_decode_frame_legacy(const vtb_genk_code_t* code, const uint8_t* cod
     vtb::Ctx& c = vtb::g_ctx;
     int r = vtb::ctx_ready(c, size_t(segments), size_t(info / 8));
     if (r != VTB_OK) return r;
-    if (hipMemcpyAsync(c.d_seg, coded, size_t(segments), hipMemcpyHostToDevice, c.stream) != hipSuccess)
+    if (hipMemcpyAsync(c.d_seg, coded, size_t(segments), hipMemcpyHostToDevice, c.stream) != hipSuccess) {
+        (void)hipStreamSynchronize(c.stream);
         return VTB_ERR_DEVICE;
+    }
     r = vtb_genk_decode_device(code, int32_t(info), c.d_seg, size_t(segments), c.d_out, size_t(info / 8), 1, c.stream);
     if (r != VTB_OK) {
         (void)hipStreamSynchronize(c.stream);
         return r;
     }
     if (hipMemcpyAsync(out, c.d_out, size_t(info / 8), hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
-        hipStreamSynchronize(c.stream) != hipSuccess)
+        hipStreamSynchronize(c.stream) != hipSuccess) {
+        (void)hipStreamSynchronize(c.stream);
         return VTB_ERR_DEVICE;
+    }
     return int(info / 8);
 }
 
