@@ -146,6 +146,21 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     A = m, B = vw.x ^ vw.y;
     return;
 #endif
+#ifdef VTB_EXP_SWZ
+    // measurement only: the cross-row partners through the LDS crossbar instead of the VALU
+    // (lane XOR 16 by ds_swizzle's bit mode; with VTB_EXP_SWZ >= 2 also XOR 32 by ds_bpermute)
+    if constexpr (P == 4) {
+        A = m + vw.x;
+        B = uint32_t(__builtin_amdgcn_ds_swizzle(int(m), 0x401F)) + vw.y;
+        return;
+    }
+    if constexpr (P == 5 && VTB_EXP_SWZ >= 2) {
+        const int x32 = int((__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ^ 32u) << 2);
+        A = m + vw.x;
+        B = uint32_t(__builtin_amdgcn_ds_bpermute(x32, int(m))) + vw.y;
+        return;
+    }
+#endif
     if constexpr (P == 4 || P == 5) {
         if constexpr (P == 4) {
             asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"

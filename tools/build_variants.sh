@@ -34,6 +34,8 @@ for v in "$@"; do
     bitop3) build bitop3 -DVTB_EXP_BITOP3 ;;
     rd1) build rd1 -DVTB_EXP_RD1 ;;
     tab32) build tab32 -DVTB_EXP_TAB32 ;;
+    swz16) build swz16 -DVTB_EXP_SWZ=1 ;;
+    swz) build swz -DVTB_EXP_SWZ=2 ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
