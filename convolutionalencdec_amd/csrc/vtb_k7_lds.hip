@@ -967,8 +967,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 
 // Renormalisation: reference = location 0 (lane 0) at a step whose history is clear, the
 // subtraction folded into the history clear (soft: every 12 steps; hard: once per chunk).
-#define VTB_RENORM_READ(I) (SOFT ? ((I) % 12) == 10 : (I) == 40)
-#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % 12) == 11 : (I) == 47)
+#ifndef VTB_EXP_RN
+#define VTB_EXP_RN 12  // soft renormalisation period in steps (12, 16 or 24: divides the chunk)
+#endif
+#define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)
+#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
         if (VTB_RENORM_READ(I)) {                                                                \

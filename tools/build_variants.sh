@@ -36,6 +36,7 @@ for v in "$@"; do
     tab32) build tab32 -DVTB_EXP_TAB32 ;;
     swz16) build swz16 -DVTB_EXP_SWZ=1 ;;
     swz) build swz -DVTB_EXP_SWZ=2 ;;
+    rn16) build rn16 -DVTB_EXP_RN=16 ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
