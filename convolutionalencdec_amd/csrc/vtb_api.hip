@@ -821,7 +821,9 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
         vtb_stream_destroy(s);
         return VTB_ERR_NOMEM;
     }
-    if (hipMemset(s->d_state, 0, waves * sw * 4) != hipSuccess) {
+    // completed before returning: the calls run on the caller's streams, which a null-stream
+    // memset does not order when they are non-blocking
+    if (hipMemset(s->d_state, 0, waves * sw * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         vtb_stream_destroy(s);
         return VTB_ERR_DEVICE;
     }
@@ -978,7 +980,11 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
                 plan->seg9_ws = nullptr;
                 return lat_undo(plan, VTB_ERR_NOMEM);
             }
-            if (hipMemset(plan->seg9_ws, 0, 256) != hipSuccess) return lat_undo(plan, VTB_ERR_DEVICE);  // arrival counter
+            // the arrival counter, zeroed in stream order before the first SEG launch (a plain
+            // hipMemset runs on the null stream, which does not order the non-blocking plan
+            // stream: a launch could add to the counter before the zero landed, so that no
+            // workgroup is elected and the completion word is never written)
+            if (hipMemsetAsync(plan->seg9_ws, 0, 256, plan->stream) != hipSuccess) return lat_undo(plan, VTB_ERR_DEVICE);
             plan->seg9_wgs = wgs;
             plan->seg9_waves = w9;
         }

@@ -109,14 +109,17 @@ int tb_block(int T) {
     return (per + 47) / 48 * 48;
 }
 int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
-// SPLIT: frame A's half ends at t1 (a multiple of 48), frame B's starts kSplitWarm steps
-// earlier, and both run t1 steps: t1 = the smallest multiple of 48 with 2 t1 - kSplitWarm >= T.
+// SPLIT: frame A's half ends at t1 (a multiple of 48), frame B's starts `warm` steps
+// earlier, and both run t1 steps: t1 = the smallest multiple of 48 with 2 t1 - warm >= T
+// (ceil((T + warm) / 2): with the floor, T + warm odd and (T + warm - 1) / 2 a multiple of 48
+// left frame B one step short of T - 1 -- fixed in round 2, tests/test_gpu_parity.py
+// test_split_frames_vs_oracle L = 1051, 2203 and test_split_loop_odd_tail).
 // kSplitWarm = 96: frame B's metrics then equal frame A's up to a constant at t1 in all of
 // 2,000 simulated soft frames at SNR -5 dB (48: 98.2 %, and every miss costs its wave a
 // second, unsplit pass).
 constexpr int kSplitWarm = 96;
 __host__ __device__ constexpr int split_t1(int T, int warm = kSplitWarm) {
-    return ((T + warm) / 2 + kChunk - 1) / kChunk * kChunk;
+    return ((T + warm + 1) / 2 + kChunk - 1) / kChunk * kChunk;
 }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.

@@ -114,12 +114,14 @@ def test_soft_random_vs_oracle(orc, K, L, kernel):
 
 
 @pytest.mark.parametrize("soft", [False, True])
-@pytest.mark.parametrize("L", [234, 235, 500, 1519, 2970])
+@pytest.mark.parametrize("L", [234, 235, 500, 1051, 1519, 2203, 2970])
 def test_split_frames_vs_oracle(orc, L, soft):
     """Small K=7 batches decode each frame in one wave as two halves at once (DESIGN.md 4.1,
     split frames): the frame-length limits of that mode (T = 240, t1 = 1536), clean, noisy and
     pure-noise frames (the halves' metrics then rarely converge: the unsplit re-decode), an
-    odd count, and one frame alone -- against the oracle."""
+    odd count, and one frame alone -- against the oracle.  L = 1051 and 2203 (T = 1 mod 96):
+    T + 96 odd with (T + 95) / 2 a multiple of 48, where a floored t1 left the second half one
+    step short of the frame's end (found by the round-2 fuzz sweep, seed 31337 case 1947)."""
     K = 7
     code = ConvCode(K, CODES[K])
     d = ViterbiDecoder(code, frame_bits=L, soft=soft)
@@ -131,6 +133,26 @@ def test_split_frames_vs_oracle(orc, L, soft):
         want = orc.decode(K, CODES[K], x, L, soft=soft)
         assert (dev_decode(d, x) == want).all(), (L, soft, seed)
         assert (dev_decode(d, x[:1]) == want[:1]).all(), (L, soft, seed)
+
+
+@pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("L", [1915, 2059])
+@pytest.mark.parametrize("kernel", ["auto", "k7s"], indirect=True)
+def test_split_loop_odd_tail(orc, L, soft, kernel):
+    """The persistent split kernel at frame lengths where a floored t1 left
+    the second half one step short of T - 1: L = 1915 (T = 1 mod 96, warm-up 96; the kernel
+    decodes it) and L = 2059 (T = 49 mod 96, warm-up 48: with the correct t1 its halves no
+    longer fit 8 waves per CU, so the global-survivor variant decodes it).  Soft input takes
+    the split kernel by default, hard input under k7s."""
+    K, F = 7, 4096
+    if soft:
+        unc, x = random_frames(orc, K, L, F, 0.0, 880 + L, soft=True, sigma=0.55)
+    else:
+        unc, x = random_frames(orc, K, L, F, 0.03, 880 + L)
+    want = orc.decode(K, CODES[K], x, L, soft=soft, threads=16)
+    got = dev_decode(ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft), x)
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (L, soft, bad.size, bad[:8])
 
 
 @pytest.mark.parametrize("soft", [False, True])
