@@ -682,23 +682,26 @@ __device__ __forceinline__ void load_raw0(const uint8_t* in, size_t in_stride, s
 }
 
 // The same for the persistent split kernel: chunk 0 of both halves of frame f (A from step 0,
-// B from step t1 - warm).
+// B from step t1 - warm).  Plain loads, not asm: the split kernel's convergence branch sits
+// between this prefetch and its use, and the register allocator copied asm-loaded registers
+// at that join before the asm wait, i.e. while the loads were still in flight (rare,
+// timing-dependent wrong frames, found by the round-2 fuzz sweep); for compiler-visible loads
+// the compiler places the wait before any use, copies included.
 template <bool SOFT>
 __device__ __forceinline__ void load_raw0_split(const uint8_t* in, size_t in_stride, int T, int t1, int warm, size_t f,
                                                 uint32_t& ra, uint32_t& rb) {
     const int lane = threadIdx.x, srow = lane < kChunk ? lane : lane - kChunk;
     constexpr uint32_t SB = SOFT ? 2 : 1;
     const uint8_t* a = in + f * in_stride;
-    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(a));
-    const uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(a + SB * size_t(t1 - warm)));
+    const uint8_t* b = a + SB * size_t(t1 - warm);
     const int Tb = T - t1 + warm;
     const uint32_t tc = SB * uint32_t(srow < T ? srow : T - 1), tcb = SB * uint32_t(srow < Tb ? srow : Tb - 1);
     if constexpr (SOFT) {
-        asm volatile("global_load_ushort %0, %2, %4\n\tglobal_load_ushort %1, %3, %5"
-                     : "=&v"(ra), "=&v"(rb) : "v"(tc), "v"(tcb), "s"(baseA), "s"(baseB));
+        ra = *reinterpret_cast<const unsigned short*>(a + tc);
+        rb = *reinterpret_cast<const unsigned short*>(b + tcb);
     } else {
-        asm volatile("global_load_ubyte %0, %2, %4\n\tglobal_load_ubyte %1, %3, %5"
-                     : "=&v"(ra), "=&v"(rb) : "v"(tc), "v"(tcb), "s"(baseA), "s"(baseB));
+        ra = a[tc];
+        rb = b[tcb];
     }
 }
 

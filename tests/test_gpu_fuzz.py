@@ -40,7 +40,13 @@ def _cases(n=FUZZ_N or 128, seed=FUZZ_SEED or 20261016):
     out = []
     for i in range(n):
         K = int(rng.choice([3, 5, 7, 7, 7, 7, 9, 9]))
-        L = int(rng.choice([1, 8, 57, 200, 234, 500, 1024, 1519, 2048, 3000, 4100]))
+        # half the cases at the listed lengths (mode limits), half at any length: the split and
+        # segment geometries depend on T modulo 48 and 96 (a floored split point once left the
+        # second half of a frame one step short at T = 1 mod 96)
+        if rng.integers(0, 2):
+            L = int(rng.choice([1, 8, 57, 200, 234, 500, 1024, 1519, 2048, 3000, 4100]))
+        else:
+            L = int(rng.integers(1, 4200))
         if K == 9 and L > 2048:
             L = 2048
         if K in (3, 5) and L > 2048:
