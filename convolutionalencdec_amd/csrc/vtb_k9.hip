@@ -608,6 +608,11 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     const uint32_t wlane = 4u * rev6(lam);  // survivor word byte offset of the lane within a column
     uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4], msave[4] = {0, 0, 0, 0};
     const int tacs = (dbg & 2) ? 0 : SEG ? sg->n : Tpad;
+    // STREAM, soft, last call with odd T: the window of step T - 1 (the last real step, even)
+    // also holds padding step T, whose ACS runs on clamped input; the metrics right after step
+    // T - 1 hold each location's own even decision (bit 0 of each half), kept in msave for the
+    // survivor fix-up below (the ACS of step T may carry another location's bit 0 into l)
+    const int tsave = (STREAM && SOFT && sa.last && (T & 1)) ? T - 1 : -1;
     for (int t0 = tbeg; t0 < tacs; t0 += kCh) {
         const int c0 = t0 / kCh;
         // survivor column of step t0 (streaming: position in the ring)
@@ -641,6 +646,11 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) M[r] = pk_min(A[r], Bc[r]);
+            if constexpr (STREAM && SOFT && (I & 1) == 0) {
+                if (t0 + I == tsave)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) msave[r] = M[r];
+            }
             if constexpr (!SOFT && (I & 7) == 7) {
                 // octet history bytes: [A oct 0, A oct 1, B oct 0, B oct 1] per 16 steps
 #pragma unroll
@@ -728,7 +738,8 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
 #pragma unroll
             for (int r = 0; r < 4; r++) sa.state[wp * kStreamStateWords9 + 64 * r + lane] = M[r];
         // Soft input, last call, padding steps [T, Tpad): own-keeping survivor bits, one bit per
-        // step (T may be odd: the window of step T - 1 keeps its real even-step bit)
+        // step.  For odd T the window of step T - 1 gets the location's own even decision
+        // (msave, captured after step T - 1), not the bit step T's ACS carried in.
         if (SOFT && sa.last) {
             uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + slot * ws_wave);
             for (int g = T >> 4; g < (Tpad >> 4); g++) {
@@ -743,6 +754,11 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                     }
                     own |= own << 16;
                     mask |= mask << 16;
+                    if ((T & 1) && ((T - 1) >> 4) == g) {
+                        const int w = ((T - 1) & 15) >> 1, bit = 8 * (w & 1) + 2 * (w >> 1);
+                        own |= ((msave[r] & 1u) << bit) | (((msave[r] >> 16) & 1u) << (bit + 16));
+                        mask |= (1u << bit) | (1u << (bit + 16));
+                    }
                     uint32_t* p = wsw + (kColBytes / 4) * ((16 * g % sa.ring) >> 4) + (wlane >> 2) + 64 * rev2(r);
                     *p = (*p & ~mask) | (own & mask);
                 }

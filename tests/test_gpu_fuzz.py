@@ -136,3 +136,59 @@ def test_global_survivor_variant_hard_hybrid(orc, L, noise, monkeypatch):
     want = orc.decode(7, CODES[7], x, L, threads=THREADS)
     got = ViterbiDecoder(ConvCode(7, CODES[7]), frame_bits=L).decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
     assert (got == want).all()
+
+
+def _stream_cases(n=(FUZZ_N // 8) or 24, seed=(FUZZ_SEED + 2) if FUZZ_SEED else 20261018):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        K = int(rng.choice([7, 7, 9]))
+        soft = bool(rng.integers(0, 2))
+        L = int(rng.integers(1, 6000))
+        F = int(rng.integers(1, 10))
+        noise = float(rng.choice([0.0, 0.03, 0.07, 0.5]))
+        out.append((i, K, L, F, soft, noise))
+    return out
+
+
+@pytest.mark.parametrize("case", _stream_cases(),
+                         ids=lambda c: f"{c[0]}-K{c[1]}-L{c[2]}-F{c[3]}-{'soft' if c[4] else 'hard'}-p{c[5]}")
+def test_stream_random_chunking_vs_oracle(orc, case):
+    """The streaming decoder (vtb_stream_*, K=7 and K=9) at random frame lengths, stream
+    counts, noise levels and chunkings (calls of 0 to 1,200 segments, two frames per object):
+    the bits each stream emits over a frame's calls, concatenated, equal the oracle's
+    whole-frame decode."""
+    from convolutionalencdec_amd import ViterbiStream
+
+    i, K, L, F, soft, noise = case
+    rng = np.random.default_rng(4000 + i)
+    g = CODES[K]
+    sb = 2 if soft else 1
+    T = L + K - 1
+    vs = ViterbiStream(ConvCode(K, g), streams=F, soft=soft)
+    for frame in range(2):
+        if soft:
+            sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
+            unc, x = random_frames(orc, K, L, F, 0.0, 3000 + 2 * i + frame, soft=True, sigma=sigma)
+        else:
+            unc, x = random_frames(orc, K, L, F, noise, 3000 + 2 * i + frame)
+        x = np.ascontiguousarray(x).reshape(F, -1)
+        want = np.unpackbits(orc.decode(K, g, x, L, soft=soft, threads=THREADS), axis=1)[:, :L]
+        xd = torch.from_numpy(x).cuda()
+        got = [[] for _ in range(F)]
+        pos = 0
+        while True:
+            c = int(min(T - pos, rng.integers(0, 1201)))
+            last = pos + c == T
+            out, nb = vs.push(xd[:, pos * sb:(pos + c) * sb] if c else None, last=last)
+            pos += c
+            out, nb = out.cpu().numpy(), nb.cpu().numpy()
+            assert (nb >= 0).all(), (case, frame, pos)
+            for f in range(F):
+                if nb[f] > 0:
+                    got[f].append(np.unpackbits(out[f])[:nb[f]])
+            if last:
+                break
+        for f in range(F):
+            bits = np.concatenate(got[f]) if got[f] else np.zeros(0, np.uint8)
+            assert bits.size == L and (bits == want[f]).all(), (case, frame, f)
