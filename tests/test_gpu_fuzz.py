@@ -192,3 +192,36 @@ def test_stream_random_chunking_vs_oracle(orc, case):
         for f in range(F):
             bits = np.concatenate(got[f]) if got[f] else np.zeros(0, np.uint8)
             assert bits.size == L and (bits == want[f]).all(), (case, frame, f)
+
+
+def _genk_cases(n=(FUZZ_N // 8) or 16, seed=(FUZZ_SEED + 3) if FUZZ_SEED else 20261019):
+    from helpers import GENK_CODES
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        c = int(rng.integers(0, len(GENK_CODES)))
+        k = GENK_CODES[c][0]
+        unit = 8 * k // np.gcd(8, k)  # info bits: a multiple of 8 and of k
+        L = unit * int(rng.integers(1, 3000 // unit + 1))
+        F = int(rng.choice([1, 2, 3, 17, 64, 257, 1000]))
+        p = float(rng.choice([0.0, 0.02, 0.08, 0.5]))
+        out.append((i, c, L, F, p))
+    return out
+
+
+@pytest.mark.parametrize("case", _genk_cases(), ids=lambda c: f"{c[0]}-code{c[1]}-L{c[2]}-F{c[3]}-p{c[4]}")
+def test_genk_random_vs_oracle(orc, case):
+    """The general rate-k/n decoder (vtb_genk_decode_device) at random codes of the test set,
+    frame lengths, batch sizes and BSC noise, against oracle_genk_decode."""
+    from helpers import GENK_CODES, genk_frames
+
+    from convolutionalencdec_amd import GenKDecoder
+
+    i, c, L, F, p = case
+    k, K, g = GENK_CODES[c]
+    unc, coded = genk_frames(orc, k, K, g, L, F, p, 6000 + i)
+    want = orc.genk_decode(k, K, g, coded, L)
+    got = GenKDecoder(k, K, g, L).decode_device(torch.from_numpy(coded).cuda()).cpu().numpy()
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (case, bad.size, bad[:8])
