@@ -18,12 +18,12 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC
 
 LEGACY_SRCS := $(CSRC)/legacy/convEncode.c $(CSRC)/legacy/convHelpers.c $(CSRC)/legacy/viterbiDecoder.c
 LEGACY_HDRS := include/viterbiDecoder.h include/viterbiDecoderButterflyk1.h include/convEncode.h include/convHelpers.h
-LEGACY_CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wno-unused-function
+LEGACY_CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wno-unused-function -pthread
 
 LEGACY_KS := 3 5 7 9 4_k2n3 3_k3n4
 
-.PHONY: all lib legacy oracle clean
-all: lib legacy oracle
+.PHONY: all lib legacy oracle testprogs clean
+all: lib legacy oracle testprogs
 
 lib: $(LIB)/libviterbi_amd.so
 legacy: $(foreach K,$(LEGACY_KS),$(LIB)/libviterbi_legacy_k$(K).so)
@@ -42,6 +42,15 @@ $(LIB)/libviterbi_legacy_k%.so: $(LEGACY_SRCS) $(LEGACY_HDRS) params/k%/convCode
 oracle: legacy
 	$(MAKE) -C oracle
 
+# C test programs run by the GPU tests (built here; the binaries travel with the tree)
+TESTBIN := tests/native/build
+testprogs: $(TESTBIN)/legacy_rand_mt
+
+$(TESTBIN)/legacy_rand_mt: tests/native/legacy_rand_mt.c $(LIB)/libviterbi_legacy_k7.so $(LEGACY_HDRS)
+	@mkdir -p $(TESTBIN)
+	$(CC) -O2 -std=gnu11 -Wall -pthread -Iparams/k7 -Iinclude -o $@ $< params/k7/convCodeParams.c \
+		-L$(LIB) -lviterbi_legacy_k7 -lviterbi_amd -Wl,-rpath,'$$ORIGIN/../../../convolutionalencdec_amd/lib'
+
 clean:
-	rm -rf $(LIB)/obj $(LIB)/*.so
+	rm -rf $(LIB)/obj $(LIB)/*.so $(TESTBIN)
 	$(MAKE) -C oracle clean

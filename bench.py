@@ -17,11 +17,24 @@ kernel (HIP-event time per launch on the launch stream, algorithmic bytes per la
 bytes per launch from profiles/pmc_traffic.json) and the CPU baseline (the reference's own
 decoder, oracle/_ref, timed on this host's cores at N=1).  dtype "u16": the decoder's path
 metrics are packed unsigned 16-bit integers.
+
+Launch modes (launch_plan; `--dry-run` prints the decision without touching a GPU):
+  * under torchrun (WORLD_SIZE set): one rank per GPU; WORLD_SIZE must equal --gpus.
+  * `--gpus N` (N > 1) without WORLD_SIZE: this process starts torchrun with N ranks as a
+    child (before any HIP call) and exits with its status, so `bench.py --gpus 8` alone
+    measures 8 GPUs, never silently one.
+  * `--global-frames G`: strong split of one G-frame batch, rank r decodes frames
+    [floor(G r / N), floor(G (r+1) / N)) (vtb_shard_range), e.g. config C5 = 2^20 frames.
+  * `--source gpu0`: one process; the whole batch is resident on GPU 0 and each step is one
+    vtb_decode_peer_multi call that scatters the shards over xGMI, decodes them on every GPU
+    and gathers the bytes back (SURVEY.md 8 e, the GPU0-sourced C5 variant).
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,7 +49,7 @@ K, G = 7, (0o113, 0o171)
 CODES = {5: (5, (0o23, 0o35)), 7: (7, G), 9: (9, (0o561, 0o753))}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -48,7 +61,7 @@ def parse():
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (0 = every CPU in this process's affinity mask)")
+                    help="CPU baseline threads (0 = the effective CPUs: min(affinity mask, cgroup quota))")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: step i runs on stream i mod inflight (own plan and output), so one "
                          "batch's tail overlaps the next one's start")
@@ -60,17 +73,82 @@ def parse():
                          "receives this many segments per step, one long frame per stream")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="process group for the timing barrier and max-reduction (nccl = RCCL; gloo: rehearsal)")
-    ap.add_argument("--gen", choices=("host", "device"), default="host",
-                    help="synthetic frames from numpy on the host (default) or from the device generator "
-                         "(csrc/vtb_gen.hip: no PCIe, for large batches)")
-    return ap.parse_args()
+    ap.add_argument("--gen", choices=("auto", "host", "device"), default="auto",
+                    help="synthetic frames from numpy on the host or from the device generator (csrc/vtb_gen.hip: "
+                         "no PCIe); auto = host up to 16,384 frames per GPU, device beyond")
+    ap.add_argument("--global-frames", type=int, default=0,
+                    help="strong split: one batch of this many frames over all GPUs (rank r gets frames "
+                         "[G r / N, G (r+1) / N)); 0 = --frames per GPU (weak scaling)")
+    ap.add_argument("--source", choices=("rank", "gpu0"), default="rank",
+                    help="rank: every rank generates and decodes its own shard; gpu0: one process, the batch "
+                         "resident on GPU 0, shards scattered over xGMI by vtb_decode_peer_multi each step")
+    ap.add_argument("--peer-devices", default="",
+                    help="--source gpu0: comma-separated device list (default 0..N-1; repeats allowed, e.g. "
+                         "0,0 to rehearse the staged path on one GPU)")
+    ap.add_argument("--peer-stage-all", action="store_true",
+                    help="--source gpu0: stage every shard through its own buffers and peer copies "
+                         "(VTB_PEER_STAGE_ALL), the source GPU's too")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the launch decision (and the torchrun command it would start) as JSON and exit")
+    return ap.parse_args(argv)
 
 
-def dist_env():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def dist_env(environ=None):
+    environ = os.environ if environ is None else environ
+    world = int(environ.get("WORLD_SIZE", "1"))
+    rank = int(environ.get("RANK", "0"))
+    local = int(environ.get("LOCAL_RANK", "0"))
     return world, rank, local
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, environ, argv, port=None):
+    """What this invocation does, decided before any HIP call:
+    {"mode": "run" | "spawn" | "error", "world": N, "reason": ..., "cmd": [...] (spawn)}."""
+    ws = environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        return {"mode": "error", "world": 0, "reason": f"--gpus {args.gpus} < 1"}
+    if args.source == "gpu0":
+        if ws is not None and int(ws) != 1:
+            return {"mode": "error", "world": int(ws),
+                    "reason": "--source gpu0 is one process driving every GPU; do not launch it under torchrun"}
+        return {"mode": "run", "world": 1, "reason": f"one process, GPU 0 scatters to {args.gpus} GPU(s) over xGMI"}
+    if ws is not None:
+        if int(ws) != args.gpus:
+            return {"mode": "error", "world": int(ws),
+                    "reason": f"WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a different GPU count"}
+        return {"mode": "run", "world": int(ws), "reason": "rank of an external torchrun launch"}
+    if args.gpus == 1:
+        return {"mode": "run", "world": 1, "reason": "one GPU, one process"}
+    port = free_port() if port is None else port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return {"mode": "spawn", "world": args.gpus, "reason": f"--gpus {args.gpus} without WORLD_SIZE: starting "
+                                                            f"{args.gpus} ranks under torchrun", "cmd": cmd}
+
+
+def shard_bounds(frames, shards, index):
+    """[lo, hi) of shard `index`: floor(F i / G) .. floor(F (i+1) / G), the split of
+    vtb_shard_range (include/viterbi_amd.h)."""
+    def bound(i):
+        return (frames // shards) * i + (frames % shards) * i // shards
+    return bound(index), bound(index + 1)
+
+
+def frames_for_rank(args, world, rank):
+    if args.global_frames > 0:
+        lo, hi = shard_bounds(args.global_frames, world, rank)
+        return hi - lo
+    return args.frames
+
+
+def use_device_gen(args, frames):
+    return args.gen == "device" or (args.gen == "auto" and frames > 16384)
 
 
 def shard_seed(rank, base=314):
@@ -121,40 +199,81 @@ def cgroup_cpus():
         return None
 
 
-def cpu_baseline(seconds, threads, frame_bits):
-    """Reference decoder (oracle/_ref/libref_k7.so, compiled from the reference sources) on
-    this host: the speedDecode protocol (speedDecode.c:37-116) with the workload's frame
-    length, one independent decoder state per thread.  Falls back to the oracle port."""
-    ref = os.path.join(REPO, "oracle", "_ref", "libref_k7.so")
-    pkt_bytes = frame_bits // 8
+def effective_cpus():
+    """(CPUs this process may run on, CPUs' worth of time it may use): min(affinity mask,
+    cgroup quota rounded up), and the affinity count itself."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = os.cpu_count() or 1
-    threads = avail if threads <= 0 else max(1, min(threads, avail))
-    if os.path.exists(ref):
-        lib = ctypes.CDLL(ref)
-        lib.ref_speed.restype = ctypes.c_double
-        lib.ref_speed.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int]
+    quota = cgroup_cpus()
+    eff = avail if quota is None else max(1, min(avail, int(-(-quota // 1))))
+    return eff, avail
+
+
+def cpu_flags():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("flags"):
+                    return set(line.split(":", 1)[1].split())
+    except OSError:  # pragma: no cover
+        pass
+    return set()
+
+
+AVX512_V4 = {"avx512f", "avx512bw", "avx512dq", "avx512vl", "avx512cd"}
+
+
+def ref_builds():
+    """The reference decoder builds this host can run: x86-64-v3 (AVX2) always, x86-64-v4
+    (AVX-512) when the CPU has its flags (oracle/Makefile)."""
+    d = os.path.join(REPO, "oracle", "_ref")
+    out = [("x86-64-v3 (AVX2)", os.path.join(d, "libref_k7.so"))]
+    if AVX512_V4 <= cpu_flags():
+        out.append(("x86-64-v4 (AVX-512)", os.path.join(d, "libref_k7_v4.so")))
+    return [(isa, p) for isa, p in out if os.path.exists(p)]
+
+
+def cpu_baseline(seconds, threads, frame_bits):
+    """Reference decoder (oracle/_ref/libref_k7*.so, compiled from the reference sources) on
+    this host: the speedDecode protocol (speedDecode.c:37-116) with the workload's frame
+    length, one independent decoder state per thread.  The reference's own recipe is -Ofast
+    -march=native (speedDecode/Makefile:4); the sources do not travel to the GPU box, so both
+    prebuilt ISA levels the host supports are probed for one second on one core and the faster
+    one runs the timed sample.  Threads default to the effective CPUs (min of the affinity
+    mask and the cgroup quota).  Falls back to the oracle port."""
+    pkt_bytes = frame_bits // 8
+    eff, avail = effective_cpus()
+    threads = eff if threads <= 0 else max(1, min(threads, avail))
+    builds = ref_builds()
+    if builds:
         # The reference's VITERBI_INIT prints to stdout; keep stdout for the one JSON line.
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
+            probes = []
+            for isa, path in builds:
+                lib = ctypes.CDLL(path)
+                lib.ref_speed.restype = ctypes.c_double
+                lib.ref_speed.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int]
+                probes.append((lib.ref_speed(1.0, 1, pkt_bytes), isa, lib))
+            one, isa, lib = max(probes, key=lambda p: p[0])
             mbps = lib.ref_speed(seconds, threads, pkt_bytes)
-            # SURVEY.md 8(d): also one core, at the workload's frame length and at speedDecode's
-            # own 2048-bit packets (speedDecode.c:38-47)
-            one = lib.ref_speed(min(2.0, seconds), 1, pkt_bytes)
+            # SURVEY.md 8(d): also one core at speedDecode's own 2048-bit packets (speedDecode.c:38-47)
             one_2048 = lib.ref_speed(min(2.0, seconds), 1, 256)
         finally:
             os.dup2(saved, 1)
             os.close(saved)
-        return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference",
+        return {"value": round(mbps, 2), "unit": "Mbit/s", "cores": threads, "kind": "reference", "isa": isa,
+                "isa_probe_single_core": {p[1]: round(p[0], 2) for p in probes},
                 "single_core_value": round(one, 2), "single_core_value_2048bit": round(one_2048, 2),
                 "cpu_model": cpu_model(), "host_cpus_available": avail, "cgroup_cpu_quota": cgroup_cpus(),
+                "effective_cpus": eff,
                 "sample": f"reference viterbiDecoderHardButterflyk1 (hard; the reference has no soft decoder), K=7, "
                           f"{frame_bits}-bit frames, speedDecode protocol (16 packets, srand(314)), {threads} threads x "
-                          f"{seconds:g} s, one decoder state per thread"}
+                          f"{seconds:g} s, one decoder state per thread, {isa} build"}
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from helpers import Oracle  # test infrastructure: the checker, used here only as the timed CPU leg
 
@@ -170,6 +289,7 @@ def cpu_baseline(seconds, threads, frame_bits):
         n += frames
     dt = time.perf_counter() - t0
     return {"value": round(n * frame_bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
+            "effective_cpus": eff, "host_cpus_available": avail,
             "sample": f"oracle soft decoder (C restatement), {frames} frames x {frame_bits} bits repeated for "
                       f"{seconds:g} s on {threads} threads"}
 
@@ -274,8 +394,93 @@ def stream_bench(args, dev, local, world):
     print(json.dumps(line), flush=True)
 
 
+def peer_bench(args):
+    """--source gpu0: the batch is resident on GPU 0 (produced there by the device generator,
+    as by a demodulator) and each step is one vtb_decode_peer_multi call: shard i of the
+    devices list is copied to its GPU over xGMI, decoded there on that GPU's own stream and
+    plan, and its L/8 bytes per frame copied back; GPU 0's own shard decodes in place.  The
+    call is asynchronous on GPU 0's current stream, whose completion covers every shard.
+    value = all frames' bits / step time (strong scaling over the devices list)."""
+    import torch
+
+    from convolutionalencdec_amd import ConvCode, decode_peer
+    from convolutionalencdec_amd import frames as devframes
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a ROCm GPU")
+    devs = [int(d) for d in args.peer_devices.split(",")] if args.peer_devices else list(range(args.gpus))
+    if not devs or any(d < 0 or d >= torch.cuda.device_count() for d in devs):
+        raise SystemExit(f"--peer-devices {devs}: {torch.cuda.device_count()} GPU(s) visible")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    code = ConvCode(*CODES[args.K])
+    soft = not args.hard
+    L = args.frame_bits
+    G_frames = args.global_frames if args.global_frames > 0 else args.frames * len(devs)
+    d_unc, d_rx = devframes.make_frames(code, G_frames, L, soft=soft, snr_db=args.snr_db, p=0.0559,
+                                        seed=shard_seed(0), device=0)
+    x = d_rx.reshape(G_frames, -1)
+    out = torch.empty((G_frames, (L + 7) // 8), dtype=torch.uint8, device=dev)
+
+    def step():
+        decode_peer(x, devs, code=code, frame_bits=L, soft=soft, out=out, stage_all=args.peer_stage_all)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ref = out.clone()
+    timer = Timer(1, lambda: torch.cuda.synchronize(dev), lambda: None, lambda t: t)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    elapsed = timer.run(step, args.steps, on_start=lambda: ev0.record(stream), on_end=lambda: ev1.record(stream))
+    call_ms = ev0.elapsed_time(ev1) / args.steps
+    same = bool(torch.equal(out, ref))
+    ber = float(np.unpackbits((out ^ d_unc).cpu().numpy()).mean())
+    T = L + code.S
+    in_b = (2 if soft else 1) * T
+    ob = (L + 7) // 8
+    remote = sum(hi - lo for i, d in enumerate(devs) for lo, hi in [shard_bounds(G_frames, len(devs), i)]
+                 if d != 0 or args.peer_stage_all)
+    value = G_frames * L / (elapsed / args.steps) / 1e6
+    alg = G_frames * (in_b + ob)
+    line = {"metric": METRIC, "value": round(value, 2), "unit": "Mbit/s", "n_gpus": len(set(devs)),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "strong" if args.global_frames > 0 else "weak",
+            "vs_baseline": None, "dtype": "u16", "data": "synthetic (device generator on GPU 0)",
+            "config": {"workload": f"K={args.K} r=1/2 {'8-bit soft' if soft else 'hard'}-decision Viterbi, "
+                                   f"{G_frames} frames x {L} info bits resident on GPU 0, shards over "
+                                   f"{len(devs)} device slot(s) {devs} via xGMI (vtb_decode_peer_multi)",
+                       "global_batch_frames": G_frames, "frame_bits": L, "devices": devs,
+                       "stage_all": bool(args.peer_stage_all),
+                       "parallelism": "GPU0-sourced contiguous shards, peer copies, no collective",
+                       "xgmi_bytes_per_step": remote * (in_b + ob), "outputs_stable": same, "decoded_ber": ber},
+            "roofline": {"bound": "hbm", "achieved": round(alg / (call_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                         "traffic": None, "kernel_ms": round(call_ms, 5), "algorithmic_bytes_per_launch": alg,
+                         "note": "kernel_ms spans one whole peer call on GPU 0's stream (copies + every shard's "
+                                 "decode), not one kernel"},
+            "cpu_baseline": None}
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    plan = launch_plan(args, os.environ, argv)
+    if args.dry_run:
+        print(json.dumps(plan), flush=True)
+        return 0
+    if plan["mode"] == "error":
+        print(f"bench.py: {plan['reason']}", file=sys.stderr, flush=True)
+        return 2
+    if plan["mode"] == "spawn":
+        # a child process (never exec: nothing here has touched the GPU, but the ranks must be
+        # torchrun's children so that it can tear them down); our exit status is theirs
+        print(f"bench.py: {plan['reason']}", file=sys.stderr, flush=True)
+        return subprocess.call(plan["cmd"])
+    if args.source == "gpu0":
+        return peer_bench(args)
     world, rank, local = dist_env()
     import torch
 
@@ -318,9 +523,12 @@ def main():
 
     code = CODES[args.K]
     soft = not args.hard
-    F, L = args.frames, args.frame_bits
+    F, L = frames_for_rank(args, world, rank), args.frame_bits
+    if F < 1:
+        raise SystemExit(f"rank {rank}: empty shard ({args.global_frames} frames over {world} GPUs)")
     T = L + code[0] - 1
-    if args.gen == "device":
+    device_gen = use_device_gen(args, F)
+    if device_gen:
         from convolutionalencdec_amd import frames as devframes
 
         d_unc, d_rx = devframes.make_frames(ConvCode(*code), F, L, soft=soft, snr_db=args.snr_db, p=0.0559,
@@ -419,7 +627,7 @@ def main():
     # vtb_decode_host (H2D copy, decode, D2H copy, synchronise); reported beside, never `value`.
     # Every rank at once (each GPU has its own PCIe link): aggregate over ranks, slowest rank.
     host_mbps = None
-    if args.gen == "host":
+    if not device_gen:
         rx_host = np.ascontiguousarray(rx.reshape(F, -1))
         dec.decode_host(rx_host)
         reps = 10
@@ -431,7 +639,8 @@ def main():
         host_mbps = round(world * F * L * reps / host_s / 1e6, 1)
 
     ms_per_step = elapsed / args.steps * 1e3
-    total_bits = F * L * world
+    total_frames = args.global_frames if args.global_frames > 0 else F * world
+    total_bits = total_frames * L
     value = total_bits / (elapsed / args.steps) / 1e6
     in_b = (2 if soft else 1) * T
     alg_bytes = F * (in_b + (L + 7) // 8)
@@ -463,17 +672,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_frames > 0 else "weak",
         "vs_baseline": None,
         "dtype": "u16",
-        "data": "synthetic" if args.gen == "host" else "synthetic (device generator)",
+        "data": "synthetic (device generator)" if device_gen else "synthetic",
         "config": {
             "workload": f"K={code[0]} r=1/2 {'8-bit soft' if soft else 'hard'}-decision Viterbi, {F} frames x {L} "
                         f"info bits per GPU, AWGN SNR {args.snr_db:g} dB" if soft else
                         f"K={code[0]} r=1/2 hard-decision Viterbi, {F} frames x {L} info bits per GPU, BSC p=0.0559",
             "frames_per_gpu": F,
             "frame_bits": L,
-            "global_batch_frames": F * world,
+            "global_batch_frames": total_frames,
+            "split": (f"strong: {args.global_frames} frames, contiguous shards (vtb_shard_range)"
+                      if args.global_frames > 0 else "weak: --frames per GPU"),
             "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
             "batches_in_flight": nin,
             "graph": bool(args.graph and nin == 1),
@@ -504,4 +715,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -21,6 +21,7 @@
  * prints and exit(1)s, the reference's convention for fatal configuration errors
  * (src/viterbiDecoder.c:10-13).
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,45 +43,48 @@ static vtb_genk_code_t legacy_genk_code(void) {
 /* The reference library draws nothing from rand(); the GPU runtime does (libhsa-runtime64
  * imports rand and srand).  Harnesses such as berTestK7.c build their channel from rand()
  * between decoder calls (berTestK7.c:29-43, 135-138), so every call into the GPU keeps the
- * caller's rand() stream: glibc's random state (the state array and its position word) is
- * copied before the call and put back after it, through initstate / setstate only.
- * initstate / setstate return and take the address of a state's position word, which is
- * followed by the state array (glibc random.c); the state's type is that word mod 5. */
-typedef struct {
-    int32_t* pos;      /* the caller's position word */
-    int words;         /* position word + state array */
-    int32_t saved[64]; /* their contents before the call */
-} rand_keep_t;
-static __thread int32_t rand_scratch[32]; /* a TYPE_3 state of our own (128 bytes) */
-static __thread int rand_scratch_ready;
+ * caller's rand() stream: while any decoder call is in flight, glibc's process-wide random
+ * state is switched to a private scratch state (setstate), and when the last one returns,
+ * back to the caller's.  Only the public initstate / setstate contract is used: setstate
+ * records the position of the state it leaves in that state's own first word and resumes
+ * from it on the way back, so the caller's state array and position are untouched.
+ * One process-wide mutex guards the switch and a count of calls in flight (the GPU calls
+ * themselves run concurrently); the scratch state is a process-wide static, so the global
+ * state never points at a thread's memory.  rand() draws other threads make while a
+ * decoder call is in flight come from the scratch stream. */
+static pthread_mutex_t rand_mu = PTHREAD_MUTEX_INITIALIZER;
+static int32_t rand_scratch[32]; /* a TYPE_3 state of our own (128 bytes) */
+static int rand_scratch_ready, rand_calls;
+static char* rand_caller; /* the caller's state while calls are in flight */
 
-static void rand_keep_begin(rand_keep_t* kp) {
-    static const int deg[5] = {0, 7, 15, 31, 63};
-    if (!rand_scratch_ready) { /* seed the scratch state once per thread (initstate runs 310 draws) */
-        setstate(initstate(1u, (char*)rand_scratch, sizeof(rand_scratch)));
-        rand_scratch_ready = 1;
+static void rand_keep_begin(void) {
+    pthread_mutex_lock(&rand_mu);
+    if (rand_calls++ == 0) {
+        if (!rand_scratch_ready) { /* seeds the scratch state (310 draws on it) and switches to it */
+            rand_caller = initstate(1u, (char*)rand_scratch, sizeof(rand_scratch));
+            rand_scratch_ready = 1;
+        } else {
+            rand_caller = setstate((char*)rand_scratch);
+        }
     }
-    char* cur = setstate((char*)rand_scratch); /* stores the caller's position in its state */
-    kp->pos = (int32_t*)cur;
-    const int d = deg[kp->pos[0] % 5];
-    kp->words = 1 + (d > 0 ? d : 1);
-    memcpy(kp->saved, kp->pos, (size_t)kp->words * sizeof(int32_t));
-    setstate(cur); /* back to the caller's state, unchanged */
+    pthread_mutex_unlock(&rand_mu);
 }
 
-static void rand_keep_end(rand_keep_t* kp) {
-    setstate((char*)rand_scratch); /* leave the caller's state (its position word is rewritten) */
-    memcpy(kp->pos, kp->saved, (size_t)kp->words * sizeof(int32_t));
-    setstate((char*)kp->pos); /* and return to it as it was before the call */
+static void rand_keep_end(void) {
+    pthread_mutex_lock(&rand_mu);
+    if (--rand_calls == 0) {
+        setstate(rand_caller);
+        rand_caller = NULL;
+    }
+    pthread_mutex_unlock(&rand_mu);
 }
 
-#define KEEP_RAND(call)            \
-    ({                             \
-        rand_keep_t kr_;           \
-        rand_keep_begin(&kr_);     \
-        int kr_r = (call);         \
-        rand_keep_end(&kr_);       \
-        kr_r;                      \
+#define KEEP_RAND(call)        \
+    ({                         \
+        rand_keep_begin();     \
+        int kr_r = (call);     \
+        rand_keep_end();       \
+        kr_r;                  \
     })
 
 static void gpu_failed(const char* what, int r) {

@@ -334,6 +334,12 @@ int resident_per_cu(const void* kernel, size_t lds) {
 
 hipError_t workspace_free(void* p, hipStream_t stream) { return hipFreeAsync(p, stream); }
 
+namespace {
+thread_local const char* t_last_kernel = "";
+}  // namespace
+void note_kernel(const char* name) { t_last_kernel = name; }
+const char* last_kernel() { return t_last_kernel; }
+
 unsigned long long* debug_tstamp() { return g_tstamp; }
 void set_debug_tstamp(unsigned long long* p) { g_tstamp = p; }
 
@@ -342,6 +348,12 @@ void set_debug_tstamp(unsigned long long* p) { g_tstamp = p; }
 extern "C" {
 
 const char* vtb_version(void) { return VTB_VERSION_STRING; }
+
+// Testing only (not in include/viterbi_amd.h): the kernel instance of the calling thread's last
+// decode launch ("k7_lds", "k7_lds_loop", "k7_lds_split", "k7_global", "k7_global_loop",
+// "k7_split_loop", "k9", "k9_loop", "lds_path", "k7_seg", "k9_seg", "k7_stream", "k9_stream"),
+// "" before the first.
+const char* vtb_debug_last_kernel(void) { return vtb::last_kernel(); }
 
 // Measurement only (not in include/viterbi_amd.h): device buffer of 8 u64 per wave that the
 // next K=7 frame launches fill with phase timestamps (tools/tstamp.py); nullptr turns it off.

@@ -42,6 +42,12 @@ struct Launch {
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
+// Which kernel instance the calling thread's last decode launch used (a static name such as
+// "k7_lds" or "k7_lds_loop"; vtb_debug_last_kernel).  Testing only: lets the parity tests prove
+// they ran the instance bench.py times.
+void note_kernel(const char* name);
+const char* last_kernel();
+
 // The debug timestamp buffer of the next launches (nullptr: off).  Measurement only.
 unsigned long long* debug_tstamp();
 void set_debug_tstamp(unsigned long long* p);

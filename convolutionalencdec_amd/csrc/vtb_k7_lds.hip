@@ -1481,7 +1481,9 @@ hipError_t launch_k7(const Launch& a) {
     if (GS && !a.ws) return hipErrorInvalidValue;
     const size_t lds = lds_of<GS>(a);
     size_t grid = grid_waves<GS>(a);
-    auto kern = grid < (a.frames + 1) / 2 ? kernel_of<GS, true>(a) : kernel_of<GS, false>(a);
+    const bool loop = grid < (a.frames + 1) / 2;
+    auto kern = loop ? kernel_of<GS, true>(a) : kernel_of<GS, false>(a);
+    const char* name = GS ? (loop ? "k7_global_loop" : "k7_global") : (loop ? "k7_lds_loop" : "k7_lds");
     // Batches the CUs hold at one frame per wave (up to 2 per SIMD at L = 1024) run split
     // (one frame per wave, both halves at once: k7_pair SPLIT): twice the waves, about half
     // the dependent steps per wave.  VTB_DEBUG bit 8 (measurement only): never split.
@@ -1491,8 +1493,10 @@ hipError_t launch_k7(const Launch& a) {
         if (per_cu > 0 && a.frames <= size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1)) {
             kern = ks;
             grid = a.frames;
+            name = "k7_lds_split";
         }
     }
+    note_kernel(name);
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -1560,6 +1564,7 @@ hipError_t launch_k7_split_loop(const Launch& a) {
     const int per_cu = resident_per_cu(reinterpret_cast<const void*>(kern), lds);
     size_t grid = size_t(per_cu > 0 ? per_cu : 8) * size_t(a.cus > 0 ? a.cus : 1);
     if (grid > a.frames) grid = a.frames;
+    note_kernel("k7_split_loop");
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride, a.T,
                        a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), la, nullptr, size_t(0),
                        StreamArgs());
@@ -1636,6 +1641,7 @@ hipError_t launch_k7_seg(const Launch& a, int waves, int warm, uint32_t* done) {
         if (e != hipSuccess) return e;
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
+    note_kernel("k7_seg");
     hipLaunchKernelGGL(kern, dim3(unsigned(a.frames)), dim3(64 * W), lds, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, Tpad, r0, debug_flags(), a, sg);
     return hipGetLastError();
@@ -1657,6 +1663,7 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s) {
                        : (a.soft ? k7_lds_kernel<true, true, true, false> : k7_lds_kernel<false, true, true, false>);
     const size_t lds = in_lds ? lds_l : r0;
     const size_t waves = (a.frames + 1) / 2;
+    note_kernel("k7_stream");
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
                        a.T, a.L, s.t_end, 0, int(r0), a.frames, 0, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring),
                        s);

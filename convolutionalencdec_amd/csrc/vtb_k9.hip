@@ -1125,6 +1125,7 @@ hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t
     const size_t nw = size_t(nwg) * waves, ws_wave = size_t(kColBytes) * (g.s.n / 16);
     uint8_t* words = base + 256 + nw * 512 * 4;
     auto kern = a.soft ? k9_seg_kernel<true> : k9_seg_kernel<false>;
+    note_kernel("k9_seg");
     hipLaunchKernelGGL(kern, dim3(unsigned(nwg * g.xcd)), dim3(64 * waves), lds, a.stream, a.in, a.out, a.T, a.L, delta, Tq,
                        debug_flags(), a, words, ws_wave, g);
     return hipGetLastError();
@@ -1147,6 +1148,7 @@ hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s) {
         return hipErrorInvalidValue;
     auto kern = a.soft ? k9_kernel<true, false, true> : k9_kernel<false, false, true>;
     const size_t waves = (a.frames + 1) / 2;
+    note_kernel("k9_stream");
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), (size_t)kRingBytes, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, 0, a.T, s.t_end, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws),
                        size_t(kColBytes) / 16 * size_t(s.ring), s);
@@ -1166,6 +1168,7 @@ hipError_t launch_k9(const Launch& a) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
     }
+    note_kernel(grid < (a.frames + 1) / 2 ? "k9_loop" : "k9");
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq), StreamArgs());

@@ -254,6 +254,7 @@ bool lds_path_supported(const Launch& a) {
 
 hipError_t launch_lds_path(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
+    note_kernel("lds_path");
     return a.soft ? launch_soft<true>(a) : launch_soft<false>(a);
 }
 

@@ -117,23 +117,31 @@ class ViterbiDecoder:
     def bind(self, frames, out, stream=None):
         """Validate (frames, out, stream) once and return a zero-argument callable that
         launches the decode of `frames` into `out` (vtb_decode_device) with no per-call
-        Python checks: the repeated-batch launch of a serving loop or a bench.  The caller
-        keeps both tensors alive and unchanged in shape while the callable is used."""
+        Python checks: the repeated-batch launch of a serving loop or a bench.  `frames` must
+        be contiguous (so the launcher reads the caller's own memory, never a temporary copy)
+        and `out` given; the callable holds references to both, and the caller must not
+        resize them while it is used."""
         import torch
 
+        if out is None:
+            raise ValueError("bind needs an output tensor")
+        if not frames.is_contiguous():
+            raise ValueError("bind needs contiguous frames (a reshape copy would be freed under the launcher)")
         if stream is None:
             stream = torch.cuda.current_stream(frames.device).cuda_stream
         self.decode_device(frames, out=out, stream=stream)  # validates, and warms the plan
-        x = frames.reshape(frames.shape[0], -1)
+        x = frames.reshape(frames.shape[0], -1)  # a view: frames is contiguous
         fn = native.lib().vtb_decode_device
         args = (self._plan, ctypes.c_void_p(x.data_ptr()), x.stride(0), ctypes.c_void_p(out.data_ptr()),
                 out.stride(0), x.shape[0], ctypes.c_void_p(stream))
+        keep = (frames, x, out)
 
         def launch():
             rc = fn(*args)
             if rc < 0:
                 raise native.VtbError(rc, "vtb_decode_device")
 
+        launch.tensors = keep  # the launcher owns references to the buffers it reads and writes
         return launch
 
     # -- host path ---------------------------------------------------------------------

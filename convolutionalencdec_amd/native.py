@@ -164,6 +164,13 @@ def lib():
     return L
 
 
+def last_kernel():
+    """Kernel instance of this thread's last decode launch (testing: vtb_debug_last_kernel)."""
+    f = lib().vtb_debug_last_kernel
+    f.restype, f.argtypes = ctypes.c_char_p, []
+    return f().decode()
+
+
 def strerror(code):
     try:
         return lib().vtb_strerror(int(code)).decode()

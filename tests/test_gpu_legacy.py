@@ -246,3 +246,20 @@ def test_reference_bertestk7_program_on_gpu():
     rows = [ln.split("|") for ln in out.splitlines() if ln.count("|") == 2 and ln.strip()[:1] in "-0123456789"]
     decoded_errors = tuple(int(r[2].split()[2]) for r in rows)
     assert decoded_errors == BERTEST_ERRORS, (decoded_errors, out[-2000:])
+
+
+@pytest.mark.parametrize("threads,frames", [(1, 10), (12, 15)])
+def test_rand_stream_kept_across_threads(threads, frames):
+    """many threads decoding through VITERBI_DECODER_HARD at once keep the
+    caller's glibc rand() stream (the draws after the threads continue the stream from before
+    them) and leave the process's random state where it was, not in a thread's or the
+    library's memory (tests/native/legacy_rand_mt.c, built by `make testprogs`)."""
+    import subprocess
+
+    from helpers import REPO
+
+    exe = os.path.join(REPO, "tests", "native", "build", "legacy_rand_mt")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (make testprogs)")
+    r = subprocess.run([exe, str(threads), str(frames)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout + r.stderr)[-2000:]
