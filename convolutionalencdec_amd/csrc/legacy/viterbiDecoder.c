@@ -92,12 +92,23 @@ static void gpu_failed(const char* what, int r) {
     exit(1);
 }
 
+/* k = 1 codes with n = 2 go through the rate-1/2 kernels (vtb_code_t); k = 1 codes with any
+ * other n through the general-k kernel in the reference's own uint8 butterfly arithmetic
+ * (VTB_GENK_K1_REFERENCE_U8), which vtb_code_t's two generators cannot describe. */
+#define LEGACY_K1_RATE_HALF (k == 1 && n == 2)
+
 static vtb_code_t legacy_code(void) {
     vtb_code_t c;
     c.constraint_length = K;
-    c.coded_bits = n;
+    c.coded_bits = 2;
     c.generators[0] = g[0];
-    c.generators[1] = (n > 1) ? g[n - 1] : 0; /* n != 2 is rejected by the C ABI */
+    c.generators[1] = (n > 1) ? g[n > 1 ? 1 : 0] : 0; /* used only when n == 2 */
+    return c;
+}
+
+static vtb_genk_code_t legacy_k1n_code(void) {
+    vtb_genk_code_t c = legacy_genk_code();
+    c.flags = VTB_GENK_K1_REFERENCE_U8;
     return c;
 }
 
@@ -186,10 +197,21 @@ DEFINE_ARGMIN(argmin64, 64)
 
 void viterbiInitButterflyk1(viterbiHardState_t* state) {
     printf("Specialized Viterbi Decoder for k=1\n");
-    vtb_code_t c = legacy_code();
-    uint8_t symm[1 << (VTB_MAX_K - 2)];
-    if (vtb_edge_table(&c, symm) == VTB_OK) {
-        for (unsigned i = 0; i < NUM_STATES / 2 && i < sizeof(symm); i++) state->edgeCodedBitsSymm[i] = symm[i];
+    if (LEGACY_K1_RATE_HALF) {
+        vtb_code_t c = legacy_code();
+        uint8_t symm[1 << (VTB_MAX_K - 2)];
+        if (vtb_edge_table(&c, symm) == VTB_OK) {
+            for (unsigned i = 0; i < NUM_STATES / 2 && i < sizeof(symm); i++) state->edgeCodedBitsSymm[i] = symm[i];
+        }
+        return;
+    }
+    /* any n: the table of viterbiInitButterflyk1.c:24-29 from the drop-in's own encoder */
+    convEncoderState_t enc;
+    for (unsigned i = 0; i < NUM_STATES / 2; i++) {
+        resetConvEncoder(&enc);
+        initConvEncoder(&enc);
+        enc.tappedDelay = (TAPPED_DELAY_TYPE)i;
+        state->edgeCodedBitsSymm[i] = (EDGE_METRIC_INDEX_TYPE)convEncOneInput(&enc, 0);
     }
 }
 
@@ -208,8 +230,14 @@ static int decode_staged(viterbiHardState_t* VTB_LEGACY_RESTRICT state, const ui
         printf("viterbi: frame of %d segments is not longer than the %d tail segments; nothing decoded\n", segments, S);
         return 0;
     }
-    vtb_code_t c = legacy_code();
-    int r = KEEP_RAND(vtb_decode_frame_legacy(&c, frame, segments, uncoded));
+    int r;
+    if (LEGACY_K1_RATE_HALF) {
+        vtb_code_t c = legacy_code();
+        r = KEEP_RAND(vtb_decode_frame_legacy(&c, frame, segments, uncoded));
+    } else {
+        vtb_genk_code_t c = legacy_k1n_code();
+        r = KEEP_RAND(vtb_genk_decode_frame_legacy(&c, frame, segments, uncoded));
+    }
     if (r < 0) gpu_failed("decode", r);
     return r;
 }
@@ -228,9 +256,15 @@ int viterbiDecoderHardButterflyk1(viterbiHardState_t* VTB_LEGACY_RESTRICT state,
         memcpy(staged + state->iteration, codedSegments, (size_t)segmentsIn);
         if (segmentsIn > 0) {
             /* the reference's uint8 metric update and renormalisation phase (:101-191) */
-            vtb_code_t c = legacy_code();
             uint32_t counter = state->renormCounter;
-            int r = KEEP_RAND(vtb_legacy_metrics_k1(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter));
+            int r;
+            if (LEGACY_K1_RATE_HALF) {
+                vtb_code_t c = legacy_code();
+                r = KEEP_RAND(vtb_legacy_metrics_k1(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter));
+            } else {
+                vtb_genk_code_t c = legacy_k1n_code();
+                r = KEEP_RAND(vtb_legacy_metrics_k1n(&c, codedSegments, segmentsIn, (uint8_t*)state->nodeMetricsA, &counter));
+            }
             if (r != VTB_OK) gpu_failed("metric update", r);
             state->renormCounter = counter;
         }

@@ -36,8 +36,16 @@ uint32_t gen_rev(uint64_t v, int bits) {  // convEncode.c:163-174
 
 struct GenArgs {
     int k, S, n, N, T, L, R;
+    int u8;          // VTB_GENK_K1_REFERENCE_U8: the reference's k=1 butterfly arithmetic (below)
     uint32_t rg[8];  // generators bit-reversed over k*K bits (convEncode.c:163-174)
 };
+
+// Wave-wide minimum of one value per lane (the U8 renormalisation, every 121 steps).
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, uint32_t(__shfl_xor(int(v), o)));
+    return v;
+}
 
 struct GenLayout {  // LDS byte offsets
     size_t tab, met, inb, outb, dec, total;
@@ -49,15 +57,21 @@ GenLayout gen_layout(int N, int E, int T, int L, int R, int k, bool gdec) {
     l.met = l.dec + (gdec ? 0 : 8 * size_t(T) * R * k);   // 2 * N int32
     l.tab = l.met + 8 * size_t(N);                   // N * E bytes
     l.inb = (l.tab + size_t(N) * E + 15) & ~size_t(15);  // T bytes
-    l.outb = (l.inb + size_t(T) + 15) & ~size_t(15);     // L / 8 bytes
-    l.total = (l.outb + size_t(L / 8) + 15) & ~size_t(15);
+    l.outb = (l.inb + size_t(T) + 15) & ~size_t(15);     // ceil(L / 8) bytes
+    l.total = (l.outb + size_t((L + 7) / 8) + 15) & ~size_t(15);
     return l;
 }
 
 // N <= 64 states: one state per lane, its metric in a register, the 2^k predecessors gathered
 // with ds_bpermute, the lane's 2^k edge labels (time-invariant) in registers; k is a template
 // parameter so every per-edge loop is unrolled.
-template <int KB>
+//
+// U8 (k = 1 only): the reference's k=1 butterfly arithmetic (viterbiDecoderButterflyk1.c:101-183)
+// -- the upper predecessor's branch metric is n minus the lower's, whatever the generators
+// (:104-107), sums wrap mod 256 (uint8 METRIC_TYPE), the strict '>' keeps the lower predecessor
+// on ties (:129-130), and when the counter reaches 120 the minimum is subtracted (:159-183) --
+// so that codes whose uint8 sums can wrap (n >= 4) decode exactly as the reference does.
+template <int KB, bool U8 = false>
 __device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
                                        int32_t* met, uint64_t* dec, int lane) {
     constexpr int E = 1 << KB;
@@ -70,17 +84,30 @@ __device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb,
     for (int e = 0; e < E; e++) {
         const int src = live ? (d >> KB) | (e << (kS - KB)) : 0;
         srcl[e] = src << 2;
-        lab[e] = live ? uint32_t(tab[(src << KB) | (d & (E - 1))]) : 0u;
+        if (U8)  // butterfly j = d >> 1: symm[j] = label of delay (j << 1) | 0, complemented for ec
+            lab[e] = live ? uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u) : 0u;
+        else
+            lab[e] = live ? uint32_t(tab[(src << KB) | (d & (E - 1))]) : 0u;
     }
+    uint32_t renorm = 0;
     for (int t = 0; t < T; t++) {
         const uint32_t rx = inb[t] & nmask;
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
         for (int e = 0; e < E; e++) {
-            const uint32_t pm = uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], m)) + uint32_t(__popc(lab[e] ^ rx));
+            uint32_t pm = uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], m)) + uint32_t(__popc(lab[e] ^ rx));
+            if (U8) pm &= 0xFFu;
             best = min(best, (pm << 4) | uint32_t(e));
         }
         m = int32_t(best >> 4);
+        if (U8) {
+            if (renorm >= 120) {
+                m -= int32_t(wave_min(live ? uint32_t(m) : 0xFFu));
+                renorm = 0;
+            } else {
+                renorm++;
+            }
+        }
         const int be = int(best & 15u);
 #pragma unroll
         for (int j = 0; j < KB; j++) {
@@ -93,7 +120,7 @@ __device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb,
 // N = 256 states (k * S = 8: k = 1, 2 or 4), four states per lane: d = 64 r + lane.  The
 // 4 * 2^k edge labels of a lane's states are time-invariant and sit in registers (compile-time
 // indices: k is a template parameter), the previous metrics in LDS (double-buffered).
-template <int KB>
+template <int KB, bool U8 = false>
 __device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
                                        int32_t* met, uint64_t* dec, int lane) {
     constexpr int E = 1 << KB, kS = 8, N = 256;
@@ -104,22 +131,30 @@ __device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* i
         const int d = r * 64 + lane;
         sbase[r] = d >> KB;
 #pragma unroll
-        for (int e = 0; e < E; e++) lab[r][e] = uint32_t(tab[(((d >> KB) | (e << (kS - KB))) << KB) | (d & (E - 1))]);
+        for (int e = 0; e < E; e++) {
+            if (U8)  // the butterfly identity of acs_r1 U8
+                lab[r][e] = uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u);
+            else
+                lab[r][e] = uint32_t(tab[(((d >> KB) | (e << (kS - KB))) << KB) | (d & (E - 1))]);
+        }
     }
     int cur = 0;
+    uint32_t renorm = 0;
     for (int t = 0; t < T; t++) {
         const uint32_t rx = inb[t] & nmask;
         const int32_t* mc = met + cur * N;
         int32_t* mn = met + (cur ^ 1) * N;
+        uint32_t nm[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
             for (int e = 0; e < E; e++) {
-                const uint32_t pm = uint32_t(mc[sbase[r] | (e << (kS - KB))]) + uint32_t(__popc(lab[r][e] ^ rx));
+                uint32_t pm = uint32_t(mc[sbase[r] | (e << (kS - KB))]) + uint32_t(__popc(lab[r][e] ^ rx));
+                if (U8) pm &= 0xFFu;
                 best = min(best, (pm << 4) | uint32_t(e));
             }
-            mn[r * 64 + lane] = int32_t(best >> 4);
+            nm[r] = best >> 4;
             const int be = int(best & 15u);
 #pragma unroll
             for (int j = 0; j < KB; j++) {
@@ -127,6 +162,18 @@ __device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* i
                 if (lane == j) dec[(size_t(t) * 4 + r) * KB + j] = w;
             }
         }
+        if (U8) {
+            if (renorm >= 120) {
+                const uint32_t mn4 = wave_min(min(min(nm[0], nm[1]), min(nm[2], nm[3])));
+#pragma unroll
+                for (int r = 0; r < 4; r++) nm[r] -= mn4;
+                renorm = 0;
+            } else {
+                renorm++;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) mn[r * 64 + lane] = int32_t(nm[r]);
         cur ^= 1;
         __syncthreads();
     }
@@ -159,7 +206,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     }
     const uint8_t* row = in + f * in_stride;
     for (int i = lane; i < T; i += 64) inb[i] = row[i];
-    for (int i = lane; i < a.L / 8; i += 64) outb[i] = 0;
+    for (int i = lane; i < (a.L + 7) / 8; i += 64) outb[i] = 0;
     const int32_t init = int32_t(uint8_t(N + 1));
     for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
     __syncthreads();
@@ -168,14 +215,22 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     // metric and the first minimum (lowest e among equal metrics, the reference's argmin).
     if (R == 1) {
         switch (k) {
-            case 1: acs_r1<1>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
+            case 1:
+                if (a.u8)
+                    acs_r1<1, true>(N, kS, T, inb, nmask, tab, met, dec, lane);
+                else
+                    acs_r1<1>(N, kS, T, inb, nmask, tab, met, dec, lane);
+                break;
             case 2: acs_r1<2>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
             case 3: acs_r1<3>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
             default: acs_r1<4>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
         }
         __syncthreads();
     } else if (k == 1) {
-        acs_r4<1>(a, T, inb, nmask, tab, met, dec, lane);
+        if (a.u8)
+            acs_r4<1, true>(a, T, inb, nmask, tab, met, dec, lane);
+        else
+            acs_r4<1>(a, T, inb, nmask, tab, met, dec, lane);
     } else if (k == 2) {
         acs_r4<2>(a, T, inb, nmask, tab, met, dec, lane);
     } else {
@@ -241,7 +296,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     }
     __syncthreads();
     uint8_t* orow = out + f * out_stride;  // (GDEC: each lane read the decision words its walks need)
-    for (int i = lane; i < a.L / 8; i += 64) orow[i] = outb[i];
+    for (int i = lane; i < (a.L + 7) / 8; i += 64) orow[i] = outb[i];
 }
 
 }  // namespace
@@ -258,12 +313,15 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     if (k * S > 8 || k * K > 12) return VTB_ERR_UNSUPPORTED;  // N <= 256 states, N * 2^k <= 4096 labels
     for (int i = 0; i < n; i++)
         if (code->generators[i] == 0 || (code->generators[i] >> (k * K))) return VTB_ERR_INVALID;
-    if (info_bits < 8 || info_bits % 8 || info_bits % k) return VTB_ERR_INVALID;
+    if (code->flags & ~int32_t(VTB_GENK_K1_REFERENCE_U8)) return VTB_ERR_INVALID;
+    const bool u8 = code->flags & VTB_GENK_K1_REFERENCE_U8;
+    if (u8 && k != 1) return VTB_ERR_INVALID;
+    if (info_bits < 1 || info_bits % k || info_bits > VTB_MAX_FRAME_BITS) return VTB_ERR_INVALID;
     const int T = info_bits / k + S, N = 1 << (k * S), E = 1 << k, R = (N + 63) / 64;
-    if (in_stride < size_t(T) || out_stride < size_t(info_bits / 8)) return VTB_ERR_INVALID;
+    if (in_stride < size_t(T) || out_stride < size_t((info_bits + 7) / 8)) return VTB_ERR_INVALID;
     if (frames == 0) return VTB_OK;
     vtb::GenArgs a{};
-    a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R;
+    a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R, a.u8 = u8 ? 1 : 0;
     for (int i = 0; i < n; i++) a.rg[i] = vtb::gen_rev(code->generators[i], k * K);
     // decision words in LDS while they leave room for 4 waves per CU, else in a workspace
     const size_t dec_bytes = 8 * size_t(T) * R * k;
@@ -271,6 +329,7 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, R, k, gdec);
     if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
+    vtb::note_kernel("genk");
     if (!gdec) {
         if (ly.total > 64 * 1024 &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(vtb::genk_kernel<false>),

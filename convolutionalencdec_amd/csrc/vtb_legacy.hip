@@ -250,6 +250,26 @@ int vtb_legacy_metrics_k1(const vtb_code_t* code, const uint8_t* segments, int32
     return VTB_OK;
 }
 
+int vtb_legacy_metrics_k1n(const vtb_genk_code_t* code, const uint8_t* segments, int32_t count, uint8_t* metrics,
+                           uint32_t* renorm_counter) {
+    if (!code || !metrics || !renorm_counter || count < 0 || (count > 0 && !segments)) return VTB_ERR_INVALID;
+    const int K = code->constraint_length, n = code->coded_bits;
+    if (code->input_bits != 1 || n < 1 || n > 8) return VTB_ERR_INVALID;
+    if (K < VTB_MIN_K || K > VTB_MAX_K) return VTB_ERR_UNSUPPORTED;
+    for (int i = 0; i < n; i++)
+        if (code->generators[i] >> K) return VTB_ERR_INVALID;
+    if (count == 0) return VTB_OK;
+    vtb::FwdArgs a{};
+    a.butterfly = 1, a.k = 1, a.S = K - 1, a.n = n, a.N = 1 << (K - 1), a.count = count;
+    for (int i = 0; i < n; i++) a.rg[i] = vtb::rev_bits(code->generators[i], K);
+    uint32_t m[256];
+    for (int s = 0; s < a.N; s++) m[s] = metrics[s];
+    int r = vtb::run_forward(a, segments, m, nullptr, renorm_counter);
+    if (r != VTB_OK) return r;
+    for (int s = 0; s < a.N; s++) metrics[s] = uint8_t(m[s]);
+    return VTB_OK;
+}
+
 int vtb_legacy_metrics_genk(const vtb_genk_code_t* code, const uint8_t* segments, int32_t count, uint32_t* metrics,
                             uint32_t* prev_metrics) {
     if (!code || !metrics || count < 0 || (count > 0 && !segments)) return VTB_ERR_INVALID;
@@ -269,26 +289,29 @@ int vtb_genk_decode_frame_legacy(const vtb_genk_code_t* code, const uint8_t* cod
     if (!code || !coded || !out) return VTB_ERR_INVALID;
     const int k = code->input_bits, S = code->constraint_length - 1;
     const int64_t info = int64_t(segments - S) * k;
-    if (segments <= S || info < 8 || info % 8 || info > VTB_MAX_FRAME_BITS * 8) return VTB_ERR_INVALID;
+    // k > 1: whole bytes (the reference's own requirement, viterbiDecoder.c:222-227); k = 1 any
+    // length (its butterfly decoder pads the last byte, viterbiDecoderButterflyk1.c:226-249)
+    if (segments <= S || info < 1 || (k > 1 && info % 8) || info > VTB_MAX_FRAME_BITS) return VTB_ERR_INVALID;
+    const size_t ob = size_t(info + 7) / 8;
     vtb::PrevDevice keep;
     vtb::Ctx& c = vtb::g_ctx;
-    int r = vtb::ctx_ready(c, size_t(segments), size_t(info / 8));
+    int r = vtb::ctx_ready(c, size_t(segments), ob);
     if (r != VTB_OK) return r;
     if (hipMemcpyAsync(c.d_seg, coded, size_t(segments), hipMemcpyHostToDevice, c.stream) != hipSuccess) {
         (void)hipStreamSynchronize(c.stream);
         return VTB_ERR_DEVICE;
     }
-    r = vtb_genk_decode_device(code, int32_t(info), c.d_seg, size_t(segments), c.d_out, size_t(info / 8), 1, c.stream);
+    r = vtb_genk_decode_device(code, int32_t(info), c.d_seg, size_t(segments), c.d_out, ob, 1, c.stream);
     if (r != VTB_OK) {
         (void)hipStreamSynchronize(c.stream);
         return r;
     }
-    if (hipMemcpyAsync(out, c.d_out, size_t(info / 8), hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+    if (hipMemcpyAsync(out, c.d_out, ob, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
         hipStreamSynchronize(c.stream) != hipSuccess) {
         (void)hipStreamSynchronize(c.stream);
         return VTB_ERR_DEVICE;
     }
-    return int(info / 8);
+    return int(ob);
 }
 
 }  // extern "C"

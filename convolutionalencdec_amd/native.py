@@ -19,6 +19,7 @@ VTB_ERR_DEVICE = -4
 VTB_ERR_NOMEM = -5
 
 VTB_PEER_STAGE_ALL = 1
+VTB_GENK_K1_REFERENCE_U8 = 1
 
 VTB_INPUT_HARD = 0
 VTB_INPUT_SOFT8 = 1
@@ -55,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "vtb_bsc_p32",
     "vtb_genk_decode_device",
     "vtb_legacy_metrics_k1",
+    "vtb_legacy_metrics_k1n",
     "vtb_legacy_metrics_genk",
     "vtb_genk_decode_frame_legacy",
 )
@@ -66,14 +68,14 @@ class VtbGenKCode(ctypes.Structure):
         ("input_bits", ctypes.c_int32),
         ("constraint_length", ctypes.c_int32),
         ("coded_bits", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("flags", ctypes.c_int32),  # 0 or VTB_GENK_K1_REFERENCE_U8
         ("generators", ctypes.c_uint64 * 8),
     ]
 
     @classmethod
-    def make(cls, k, K, g):
+    def make(cls, k, K, g, flags=0):
         c = cls()
-        c.input_bits, c.constraint_length, c.coded_bits = int(k), int(K), len(g)
+        c.input_bits, c.constraint_length, c.coded_bits, c.flags = int(k), int(K), len(g), int(flags)
         for i, v in enumerate(g):
             c.generators[i] = int(v)
         return c

@@ -263,15 +263,25 @@ typedef struct {
     int32_t input_bits;        /* k, 1..4 */
     int32_t constraint_length; /* K in k-bit segments; k*(K-1) <= 8 and k*K <= 12 */
     int32_t coded_bits;        /* n, 1..8 */
-    int32_t reserved;          /* 0 */
+    int32_t flags;             /* 0 or VTB_GENK_K1_REFERENCE_U8 (was `reserved`, 0) */
     uint64_t generators[8];    /* g[0..n-1], each nonzero and below 2^(k*K) */
 } vtb_genk_code_t;
 
+/* k = 1 only: decode with the reference k=1 decoder's own arithmetic
+ * (viterbiDecoderHardButterflyk1, src/viterbiDecoderButterflyk1.c:101-183) -- the butterfly
+ * identity for the upper predecessor's branch metric (n - e), uint8 metrics whose sums wrap,
+ * the strict '>' select and the subtract-the-minimum renormalisation every 121 steps -- instead
+ * of exact metrics.  The two agree whenever no uint8 sum wraps (n <= 3 with symmetric
+ * generators); for n >= 4 this mode is what reproduces the reference.  Used by
+ * the legacy drop-in for k = 1 codes with n != 2. */
+#define VTB_GENK_K1_REFERENCE_U8 1
+
 /* Hard-decision decode of `frames` rows of info_bits/k + K-1 coded segment bytes (row stride
- * in_stride) into rows of info_bits/8 bytes, MSB-first (out_stride); info_bits a multiple of
- * 8 and of k (the reference's own requirement, viterbiDecoder.c:222-227).  Device pointers,
- * asynchronous on `stream` (a hipStream_t, 0 = default) of the current device.
- * VTB_ERR_UNSUPPORTED when the trellis or the frame exceeds one CU's LDS. */
+ * in_stride) into rows of ceil(info_bits/8) bytes, MSB-first (out_stride; a partial last byte
+ * is zero-padded, as viterbiDecoderButterflyk1.c:226-249); info_bits a multiple of k, at most
+ * VTB_MAX_FRAME_BITS.  Device pointers, asynchronous on `stream` (a hipStream_t, 0 = default)
+ * of the current device.  VTB_ERR_UNSUPPORTED when the trellis or the frame exceeds one CU's
+ * LDS. */
 int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const uint8_t* d_in, size_t in_stride,
                            uint8_t* d_out, size_t out_stride, size_t frames, void* stream);
 
@@ -289,6 +299,12 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
 int vtb_legacy_metrics_k1(const vtb_code_t* code, const uint8_t* segments, int32_t count, uint8_t* metrics,
                           uint32_t* renorm_counter);
 
+/* The same update for a k = 1 code of any n (1..8 coded bits, code->input_bits == 1): the
+ * reference's butterfly with n - e as the complement (viterbiDecoderButterflyk1.c:104-107 with
+ * its compile-time n), which vtb_legacy_metrics_k1's two-generator vtb_code_t cannot describe. */
+int vtb_legacy_metrics_k1n(const vtb_genk_code_t* code, const uint8_t* segments, int32_t count, uint8_t* metrics,
+                           uint32_t* renorm_counter);
+
 /* The metric update of the generic decoder (viterbiDecoderHard, src/viterbiDecoder.c:84-131):
  * destination-indexed, exact metrics, first minimum over the 2^k predecessors.  metrics[2^(k(K-1))]
  * is updated in place; prev_metrics (optional) receives the metrics one step before the last
@@ -297,8 +313,9 @@ int vtb_legacy_metrics_genk(const vtb_genk_code_t* code, const uint8_t* segments
                             uint32_t* prev_metrics);
 
 /* One general-k hard frame of `segments` coded segments from host memory (VITERBI_DECODER_HARD
- * for k > 1): decoded by vtb_genk_decode_device, (segments - K + 1) * k / 8 bytes written to
- * out and returned (the reference's byte count for a whole frame), or a VTB_ERR_* code. */
+ * for k > 1, and for k = 1 codes with n != 2 with VTB_GENK_K1_REFERENCE_U8): decoded by
+ * vtb_genk_decode_device, ceil((segments - K + 1) * k / 8) bytes written to out and that count
+ * returned (the reference's byte count for a whole frame, :256), or a VTB_ERR_* code. */
 int vtb_genk_decode_frame_legacy(const vtb_genk_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out);
 
 #ifdef __cplusplus

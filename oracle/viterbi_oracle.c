@@ -443,7 +443,7 @@ int oracle_genk_encode(int k, int K, int n, const uint64_t* g, const uint8_t* un
 
 int oracle_genk_decode(int k, int K, int n, const uint64_t* g, const uint8_t* coded, int info_bits, uint8_t* out) {
     const int S = K - 1, kS = k * S;
-    if (k < 1 || K < 2 || n < 1 || n > 8 || kS > 16 || info_bits < 8 || info_bits % 8 || info_bits % k) return -1;
+    if (k < 1 || K < 2 || n < 1 || n > 8 || kS > 16 || info_bits < 1 || info_bits % k) return -1;
     const int N = 1 << kS, E = 1 << k, T = info_bits / k + S;
     uint64_t rg[8];
     for (int i = 0; i < n; i++) rg[i] = genk_rev(g[i], k * K);
@@ -475,7 +475,7 @@ int oracle_genk_decode(int k, int K, int n, const uint64_t* g, const uint8_t* co
         cur = nxt;
         nxt = x;
     }
-    const int nb = info_bits / 8;
+    const int nb = (info_bits + 7) / 8;
     memset(out, 0, (size_t)nb);
     int s = 0;
     for (int t = T - 1; t >= 0; t--) {
@@ -532,4 +532,57 @@ int oracle_genk_metrics(int k, int K, int n, const uint64_t* g, const uint8_t* c
     if (prev) memcpy(prev, nxt, sizeof(uint32_t) * (size_t)N);
     free(buf);
     return 0;
+}
+
+/* The reference's k = 1 decoder for any n (viterbiDecoderButterflyk1.c:82-256 with its
+ * compile-time n): symmetric edge table symm[j] = label of delay (j << 1) | 0 (:24-29), branch
+ * metric e = Hamming distance over the low n bits and its complement n - e for the upper
+ * predecessor (:104-107), uint8 sums, strict '>' select (:129-130), subtract-the-minimum
+ * renormalisation when the counter reaches 120 (:159-183), traceback from state 0 after S
+ * padding steps, MSB-first packing with the last byte zero-padded (:200-256).  Returns the
+ * reference's byte count (L - 1) / 8 + 1. */
+int oracle_k1n_decode(int K, int n, const uint64_t* g, const uint8_t* coded, int info_bits, uint8_t* out) {
+    const int S = K - 1;
+    if (K < 3 || K > 9 || n < 1 || n > 8 || info_bits < 1) return -1;
+    const int N = 1 << S, T = info_bits + S;
+    uint64_t rg[8];
+    for (int i = 0; i < n; i++) rg[i] = genk_rev(g[i], K);
+    uint8_t symm[128];
+    for (int j = 0; j < N / 2; j++) symm[j] = genk_out(n, rg, (uint64_t)j << 1);
+    uint8_t m[256], nm[256];
+    uint8_t* dec = malloc((size_t)T * N);
+    if (!dec) return -1;
+    for (int st = 0; st < N; st++) m[st] = st == 0 ? 0 : (uint8_t)(N + 1);
+    unsigned counter = 0;
+    const unsigned nmask = (1u << n) - 1u;
+    for (int t = 0; t < T; t++) {
+        for (int j = 0; j < N / 2; j++) {
+            const uint8_t em = (uint8_t)__builtin_popcount((unsigned)(symm[j] ^ coded[t]) & nmask);
+            const uint8_t ec = (uint8_t)(n - em);
+            const uint8_t a0 = (uint8_t)(m[j] + em), a1 = (uint8_t)(m[N / 2 + j] + ec);
+            const uint8_t b0 = (uint8_t)(m[j] + ec), b1 = (uint8_t)(m[N / 2 + j] + em);
+            nm[2 * j] = a0 > a1 ? a1 : a0;
+            nm[2 * j + 1] = b0 > b1 ? b1 : b0;
+            dec[(size_t)t * N + 2 * j] = a0 > a1;
+            dec[(size_t)t * N + 2 * j + 1] = b0 > b1;
+        }
+        if (counter >= 120) {
+            uint8_t mn = nm[0];
+            for (int st = 1; st < N; st++) mn = nm[st] < mn ? nm[st] : mn;
+            for (int st = 0; st < N; st++) nm[st] = (uint8_t)(nm[st] - mn);
+            counter = 0;
+        } else {
+            counter++;
+        }
+        memcpy(m, nm, (size_t)N);
+    }
+    const int nb = (info_bits - 1) / 8 + 1;
+    memset(out, 0, (size_t)nb);
+    unsigned st = 0;
+    for (int t = T - 1; t >= 0; t--) {
+        if (t < T - S && ((st & 1u) != 0)) out[t >> 3] |= (uint8_t)(0x80u >> (t & 7));
+        st = (st >> 1) | ((unsigned)dec[(size_t)t * N + st] << (S - 1));
+    }
+    free(dec);
+    return nb;
 }

@@ -36,6 +36,7 @@ class Oracle:
         L.oracle_genk_encode.argtypes = [i, i, i, v, v, i, v]
         L.oracle_genk_decode.argtypes = [i, i, i, v, v, i, v]
         L.oracle_genk_metrics.argtypes = [i, i, i, v, v, i, v, v]
+        L.oracle_k1n_decode.argtypes = [i, i, v, v, i, v]
         L.oracle_decode_hard.argtypes = [i, v, v, i, v]
         L.oracle_decode_soft.argtypes = [i, v, v, i, v]
         L.oracle_decode_batch.argtypes = [i, v, i, v, sz, i, v, sz, sz, i]
@@ -131,11 +132,25 @@ class Oracle:
     def genk_decode(self, k, K, g, frames, info_bits):
         x = np.ascontiguousarray(frames, np.uint8)
         G = (ctypes.c_uint64 * 8)(*[int(v) for v in g])
-        out = np.zeros((x.shape[0], info_bits // 8), np.uint8)
+        nb = (info_bits + 7) // 8
+        out = np.zeros((x.shape[0], nb), np.uint8)
         for f in range(x.shape[0]):
             row = np.ascontiguousarray(x[f])
-            o = np.zeros(info_bits // 8, np.uint8)
-            assert self.L.oracle_genk_decode(k, K, len(g), G, vp(row), info_bits, vp(o)) == info_bits // 8
+            o = np.zeros(nb, np.uint8)
+            assert self.L.oracle_genk_decode(k, K, len(g), G, vp(row), info_bits, vp(o)) == nb
+            out[f] = o
+        return out
+
+    def k1n_decode(self, K, g, frames, info_bits):
+        """The reference k=1 decoder for any n (oracle_k1n_decode: uint8 butterfly arithmetic)."""
+        x = np.ascontiguousarray(frames, np.uint8)
+        G = (ctypes.c_uint64 * 8)(*[int(v) for v in g])
+        nb = (info_bits + 7) // 8
+        out = np.zeros((x.shape[0], nb), np.uint8)
+        for f in range(x.shape[0]):
+            row = np.ascontiguousarray(x[f])
+            o = np.zeros(nb, np.uint8)
+            assert self.L.oracle_k1n_decode(K, len(g), G, vp(row), info_bits, vp(o)) == nb
             out[f] = o
         return out
 
@@ -272,6 +287,24 @@ GENK_CODES = (
     (2, 3, (0x2B, 0x1D, 0x37)),
 )
 GENK_REF_PARAMS = {"k4_k2n3": GENK_CODES[0], "k3_k3n4": GENK_CODES[1]}
+
+# k = 1 codes with n != 2 (params/k7n3, k9n3, k5n4): the reference decoder is generic in n
+# (viterbiDecoderButterflyk1.c:104-107); oracle/_ref/libref_<name>.so is the reference built
+# with each, tests/golden/k1n.npz its outputs.
+K1N_PARAMS = {"k7n3": (7, (0o133, 0o171, 0o165)), "k9n3": (9, (0o557, 0o663, 0o711)),
+              "k5n4": (5, (0o23, 0o35, 0o27, 0o33))}
+
+
+def k1n_frames(orc, K, g, L, F, p, seed, garbage=False):
+    """Random payloads encoded with an n-generator k=1 code (oracle_genk_encode with k = 1),
+    each coded bit flipped with probability p; garbage=True sets the unused high bits of every
+    segment byte (the reference reads only the low n bits, viterbiDecoder.c:278-281)."""
+    unc, rx = genk_frames(orc, 1, K, g, L, F, p, seed)
+    if garbage:
+        rng = np.random.default_rng(seed + 1)
+        n = len(g)
+        rx = rx | (rng.integers(0, 256, rx.shape, dtype=np.uint8) & np.uint8((0xFF << n) & 0xFF))
+    return unc, rx.astype(np.uint8)
 
 
 def legacy_layout(k, K, n):

@@ -98,7 +98,11 @@ def test_genk_abi_argument_checks():
     buf = ctypes.create_string_buffer(4096)
     c = native.VtbGenKCode.make(2, 4, (0xB5, 0x6B, 0xD9))
     call = lambda code, L, ins=600, outs=128: lib.vtb_genk_decode_device(ctypes.byref(code), L, buf, ins, buf, outs, 1, None)
-    assert call(c, 1020) == native.VTB_ERR_INVALID          # not a multiple of 8
+    assert call(c, 1021) == native.VTB_ERR_INVALID          # not a multiple of k
+    assert call(c, 16385 * 2) == native.VTB_ERR_INVALID     # past VTB_MAX_FRAME_BITS
+    assert call(native.VtbGenKCode.make(2, 4, (0xB5, 0x6B, 0xD9), native.VTB_GENK_K1_REFERENCE_U8),
+                1024) == native.VTB_ERR_INVALID            # the reference uint8 mode is k = 1 only
+    assert call(native.VtbGenKCode.make(1, 7, (0o133, 0o171, 0o165), 2), 1024) == native.VTB_ERR_INVALID  # flag
     assert call(c, 1024, ins=100) == native.VTB_ERR_INVALID  # input row too short
     assert call(native.VtbGenKCode.make(2, 4, (0x1B5, 1, 1)), 1024) == native.VTB_ERR_INVALID  # generator > 2^(kK)
     assert call(native.VtbGenKCode.make(3, 4, (0x1B5, 1, 1)), 1032) == native.VTB_ERR_UNSUPPORTED  # 512 states

@@ -1,0 +1,98 @@
+"""k = 1 codes with n != 2 on the GPU.
+
+* The legacy drop-in built for params/k7n3, k9n3 and k5n4 (libviterbi_legacy_<name>.so)
+  decodes the reference's golden frames (tests/golden/k1n.npz, produced by the reference
+  compiled with the same params) through VITERBI_DECODER_HARD exactly, with the reference's
+  byte count, and nodeMetricsCur after every 7-segment last=false chunk equals the
+  reference's (viterbiDecoderButterflyk1.c:101-191 with its compile-time n).
+* vtb_genk_decode_device with VTB_GENK_K1_REFERENCE_U8 equals the oracle's restatement
+  (oracle_k1n_decode) on random frames of any length, garbage high bits included; without
+  the flag (exact metrics) it equals oracle_genk_decode at any length.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import K1N_PARAMS, Oracle, k1n_frames, load_golden, vp
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from convolutionalencdec_amd import native  # noqa: E402
+from test_gpu_legacy import Legacy  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    if not torch.cuda.is_available() or native.lib().vtb_device_count() < 1:
+        pytest.fail("no gfx950 GPU visible to the C ABI (GPU tests must not silently pass)")
+
+
+@pytest.mark.parametrize("name", sorted(K1N_PARAMS))
+def test_legacy_dropin_decodes_reference_golden(name):
+    z = load_golden("k1n.npz")
+    leg = Legacy(name)
+    keys = sorted({k.rsplit("_", 1)[0] for k in z if k.startswith(name + "_L")})
+    assert keys
+    for key in keys:
+        L = int(key.split("_")[1][1:])
+        rx, dec = z[key + "_rx"], z[key + "_decoded"]
+        for f in range(rx.shape[0]):
+            out = np.zeros(L // 8, np.uint8)
+            assert leg.call(rx[f], out, True) == (L - 1) // 8 + 1
+            assert (out == dec[f]).all(), (name, key, f)
+
+
+@pytest.mark.parametrize("name", sorted(K1N_PARAMS))
+def test_legacy_node_metrics_after_each_chunk(name):
+    z = load_golden("k1n.npz")
+    leg = Legacy(name)
+    K, g = K1N_PARAMS[name]
+    N = 1 << (K - 1)
+    for f in range(4):
+        rx, met, dec = z[f"{name}_stream_f{f}_rx"], z[f"{name}_stream_f{f}_metrics"], z[f"{name}_stream_f{f}_decoded"]
+        reset = leg.metrics_cur()
+        assert reset[0] == 0 and (reset[1:] == (N + 1) % 256).all()
+        out = np.zeros(dec.shape, np.uint8)
+        for c in range(met.shape[0]):
+            assert leg.call(rx[7 * c:7 * (c + 1)], out, False) == 0
+            assert (leg.metrics_cur() == met[c]).all(), (name, f, c)
+        assert leg.call(rx[7 * met.shape[0]:], out, True) == dec.shape[0]
+        assert (out == dec).all(), (name, f)
+
+
+def genk_device(K, g, rx, L, flags):
+    code = native.VtbGenKCode.make(1, K, g, flags)
+    x = torch.from_numpy(np.ascontiguousarray(rx)).cuda()
+    ob = (L + 7) // 8
+    out = torch.zeros((rx.shape[0], ob), dtype=torch.uint8, device="cuda")
+    rc = native.lib().vtb_genk_decode_device(ctypes.byref(code), L, ctypes.c_void_p(x.data_ptr()), x.stride(0),
+                                             ctypes.c_void_p(out.data_ptr()), ob, rx.shape[0], None)
+    assert rc == 0, native.strerror(rc)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", sorted(K1N_PARAMS))
+@pytest.mark.parametrize("L", [1, 13, 64, 1001, 2048])
+def test_reference_u8_mode_vs_oracle(orc, name, L):
+    K, g = K1N_PARAMS[name]
+    for p, seed in ((0.0, 1), (0.06, 2), (0.5, 3)):
+        if L % 8 == 0:
+            unc, rx = k1n_frames(orc, K, g, L, 24, p, seed + L, garbage=(p == 0.06))
+        else:  # odd L: random segment bytes (any input decodes; parity is what counts)
+            unc, rx = None, np.random.default_rng(seed + 7 * L).integers(0, 256, (24, L + K - 1), dtype=np.uint8)
+        want = orc.k1n_decode(K, g, rx, L)
+        got = genk_device(K, g, rx, L, native.VTB_GENK_K1_REFERENCE_U8)
+        assert (got == want).all(), (name, L, p)
+        exact = genk_device(K, g, rx, L, 0)
+        assert (exact == orc.genk_decode(1, K, g, rx, L)).all(), (name, L, p)
+        if p == 0.0 and L % 8 == 0:
+            assert (got == unc).all()
