@@ -81,7 +81,16 @@ namespace {
 
 using namespace k7;
 
+#ifdef VTB_EXP_B128
+// measurement: rows r and r + 6 of a column adjacent (slot 12 (r / 12) + 2 (r % 6) + (r % 12) / 6),
+// so one ds_read_b128 (4 LDS cycles) replaces a ds_read2_b64 (8); 50 slots keep the column
+// bases 16-byte aligned and the eight columns of a row in distinct banks (100 dwords apart)
+constexpr int kCol = 50;
+__host__ __device__ constexpr int ring_slot(int r) { return 12 * (r / 12) + 2 * (r % 6) + (r % 12) / 6; }
+#else
 constexpr int kCol = 49;                   // 8-byte slots per table column (48 rows + bank skew)
+__host__ __device__ constexpr int ring_slot(int r) { return r; }
+#endif
 constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) columns
 #ifndef VTB_EXP_TBWARM
 #define VTB_EXP_TBWARM 48
@@ -165,13 +174,19 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     }
 #endif
     if constexpr (P == 4 || P == 5) {
+#ifdef VTB_EXP_E32
+#define VTB_ADD_ENC "v_add_u32_e32"  // measurement: the 4-byte VOP2 encoding of the add
+#else
+#define VTB_ADD_ENC "v_add_u32"
+#endif
         if constexpr (P == 4) {
-            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
+            asm volatile(VTB_ADD_ENC " %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
                          : "=&v"(A), "+v"(m) : "v"(vw.x));
         } else {
-            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 0"
+            asm volatile(VTB_ADD_ENC " %0, %1, %2\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 0"
                          : "=&v"(A), "+v"(m) : "v"(vw.x));
         }
+#undef VTB_ADD_ENC
         B = m + vw.y;
     } else {
         A = m + vw.x;
@@ -182,6 +197,14 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
         }
     }
 }
+
+#ifdef VTB_EXP_SGMASK
+__device__ __forceinline__ uint32_t sg_and(uint32_t smask, uint32_t v) {
+    uint32_t r;
+    asm("v_and_b32_e32 %0, %1, %2" : "=v"(r) : "s"(smask), "v"(v));
+    return r;
+}
+#endif
 
 // One v_bfi_b32 (the compiler otherwise splits a constant-mask select into and/and/or).
 __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b) {
@@ -863,12 +886,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // (V, W) of a slot from two unrelated VGPRs by ds_write2_b32 (a ds_write_b64 would need
     // them in a register pair: 8 moves per chunk); three bases keep offsets below 256 dwords.
     // (LDS byte addresses: the ring starts at LDS address 0, SEG: at this wave's region)
-    const uint32_t wbase0 = uint32_t(SEG ? wv * sgp->seg_bytes : 0) + 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
+    const uint32_t wbase0 = uint32_t(SEG ? wv * sgp->seg_bytes : 0) + 8u * uint32_t(ring_slot(srow)), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
     // PADCHK: the chunk may hold padding rows (only the chunk containing step T; the ACS
     // loop is split so that the check stays out of its other iterations).
     auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4], auto padchk) {
         constexpr bool PADCHK = decltype(padchk)::value;
-        uint2* col = reinterpret_cast<uint2*>(tab) + srow;  // column k at col[kCol * k]
+        uint2* col = reinterpret_cast<uint2*>(tab) + ring_slot(srow);  // column k at col[kCol * k]
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
                  "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
@@ -953,16 +976,25 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #pragma unroll
     for (int g = 0; g < AH; g++)
 #pragma unroll
-        for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * (6 * g + k));
+        for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * ring_slot(6 * g + k));
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
+#ifdef VTB_EXP_SGMASK
+    uint32_t clr_mask;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(clr_mask) : "i"(~H::MASK));
+#endif
     const int tacs = (dbg & 2) ? 0 : (SPLIT && sp ? t1s : Tpad);
     // One 48-step chunk of the ACS (fully unrolled); PADTAG: this chunk stages the chunk that
     // holds step T (padding rows possible).
     // gtag: this chunk's survivor words go to the global workspace (else LDS)
-    auto acs_chunk = [&](const int t0, auto padtag, auto gtag) __attribute__((always_inline)) {
+    // lasttag: the frame's last chunk, which may stop after ng_last of its 8 groups (the steps
+    // past T up to the chunk's end need no ACS: their survivor words are written as own-keeping
+    // patterns afterwards, pad_words) and stages nothing
+    int ng_last = 8;
+    auto acs_chunk = [&](const int t0, auto padtag, auto gtag, auto lasttag) __attribute__((always_inline)) {
         constexpr bool GSC = decltype(gtag)::value;
+        constexpr bool LASTC = decltype(lasttag)::value;
         const int c0 = t0 / kChunk;
         const uint2* ap[6];
 #pragma unroll
@@ -978,6 +1010,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #endif
 #define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)
 #define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)
+#ifdef VTB_EXP_SGMASK
+#define VTB_CLR(x) sg_and(clr_mask, (x))  // measurement: the clear mask from an SGPR, no literal
+#else
+#define VTB_CLR(x) ((x) & ~H::MASK)
+#endif
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
         if (VTB_RENORM_READ(I)) {                                                                \
@@ -990,7 +1027,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             const int w = ((I) & 15) >> 1;                                                       \
             if (w & 1) pw[w >> 1] = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
             else m_prev = M;                                                                     \
-            M = VTB_RENORM_APPLY(I) ? ((M & ~H::MASK) + dd) : (M & ~H::MASK);                    \
+            M = VTB_RENORM_APPLY(I) ? (VTB_CLR(M) + dd) : VTB_CLR(M);                            \
             if (((I) & 15) == 15) {                                                              \
                 /* bits 2j..2j+1 of byte (w & 1): window w = 2j + (w & 1) */                     \
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
@@ -1007,14 +1044,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 const uint32_t z = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
                 VTB_EXP_WORD(store_word<GSC>(dchunk, gvo, gbase, ((I) >> 4), z));                 \
             }                                                                                    \
-            M = VTB_RENORM_APPLY(I) ? ((M & ~H::MASK) + dd) : (M & ~H::MASK);                    \
+            M = VTB_RENORM_APPLY(I) ? (VTB_CLR(M) + dd) : VTB_CLR(M);                            \
         }                                                                                        \
     }
 #define VTB_GROUP(G)                                                                              \
-    {                                                                                             \
-        if ((G) == 0) load_raw(c0 + 1, ra, rb);                                                   \
-        if ((G) == 3 && VTB_EXP_STAGE) stage_compute(ra, rb, se, set, !GSC);                             \
-        if ((G) == 8 - AH && VTB_EXP_STAGE) { /* all rows of this chunk are in registers */      \
+    if (!LASTC || (G) < ng_last) {                                                                \
+        if ((G) == 0 && !LASTC) load_raw(c0 + 1, ra, rb);                                         \
+        if ((G) == 3 && VTB_EXP_STAGE && !LASTC) stage_compute(ra, rb, se, set, !GSC);            \
+        if ((G) == 8 - AH && VTB_EXP_STAGE && !LASTC) { /* all rows of this chunk are in registers */ \
             stage_write(c0 + 1, se, set, padtag);                                                 \
         }                                                                                         \
         uint2* cur = buf[(G) & 3];                                                                \
@@ -1028,11 +1065,20 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // Even groups read the next two groups' pairs of one phase (rows 6 apart in one column of
 // the ring): one ds_read2_b64 per phase and group pair, half the LDS read instructions of
 // one ds_read_b64 per step (measured 2% faster).  (VTB_EXP_RD1: one read per step.)
+#ifdef VTB_EXP_B128
+#define VTB_RD(G, k)                                                                              \
+    if (((G) & 1) == 0) {                                                                         \
+        const uint4 q_ = reinterpret_cast<const uint4*>(ap[k])[ring_slot((6 * ((G) + 2) + (k)) % kChunk) / 2]; \
+        buf[((G) + 2) & 3][k] = make_uint2(q_.x, q_.y);                                           \
+        buf[((G) + 3) & 3][k] = make_uint2(q_.z, q_.w);                                           \
+    }
+#else
 #define VTB_RD(G, k)                                                                              \
     if (((G) & 1) == 0) {                                                                         \
         buf[((G) + 2) & 3][k] = ap[k][(6 * ((G) + 2) + (k)) % kChunk];                            \
         buf[((G) + 3) & 3][k] = ap[k][(6 * ((G) + 3) + (k)) % kChunk];                            \
     }
+#endif
 #else
 #define VTB_RD(G, k)                                                                              \
     buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk], buf[(G) & 3][k]);
@@ -1062,18 +1108,52 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         else __builtin_amdgcn_s_setprio(0);
     };
     // one chunk, its survivor words to the global workspace (GS, steps before tg) or to LDS
-    auto run_chunk = [&](const int t0, auto padtag) __attribute__((always_inline)) {
+    auto run_chunk = [&](const int t0, auto padtag, auto lasttag) __attribute__((always_inline)) {
         if constexpr (GS) {
-            if (t0 < tg) acs_chunk(t0, padtag, std::true_type{});
-            else acs_chunk(t0, padtag, std::false_type{});
+            if (t0 < tg) acs_chunk(t0, padtag, std::true_type{}, lasttag);
+            else acs_chunk(t0, padtag, std::false_type{}, lasttag);
         } else {
-            acs_chunk(t0, padtag, std::false_type{});
+            acs_chunk(t0, padtag, std::false_type{}, lasttag);
         }
+    };
+    // Survivor words of the last chunk's steps [t0 + n_end, t0 + 48) (n_end = 24, all past T):
+    // every location keeps its own predecessor there (what the padding rows make the ACS
+    // decide), so a decision is the location's own bit p = 5 - (t mod 6), i.e. bit t mod 6 of
+    // l' = widx, and a walk from location 0 at Tpad stays at location 0 down to T.  The word
+    // with steps [16, 24) computed keeps those (soft: windows 0-3 in pw[0..1]; hard: octet 0 in
+    // m_prev) and takes the pattern for the rest.
+    auto pad_words = [&](const int t0, auto gtag) __attribute__((always_inline)) {
+        constexpr bool GSC = decltype(gtag)::value;
+        uint32_t* dchunk = dec + ((t0 - lds_t0) >> 4) * 64 + widx;
+        const uint32_t gvo = 4u * ((t0 >> 4) * 64 + widx);
+        auto lbit = [&](int t) { return (widx >> (t % 6)) & 1u; };
+        auto pattern = [&](int s16) {  // one frame's 16-bit half of the word of steps [s16, s16 + 16)
+            uint32_t p = 0;
+            if constexpr (SOFT) {
+#pragma unroll
+                for (int w = 0; w < 8; w++)
+                    p |= (lbit(s16 + 2 * w) | (lbit(s16 + 2 * w + 1) << 1)) << (8 * (w & 1) + 2 * (w >> 1));
+            } else {
+#pragma unroll
+                for (int b = 0; b < 16; b++) p |= lbit(s16 + b) << b;  // octets 0, 1 in bytes 0, 1
+            }
+            return p * kR1;  // both frames
+        };
+        const uint32_t p1 = pattern(t0 + 16), p2 = pattern(t0 + 32);
+        uint32_t z1;
+        if constexpr (SOFT) {
+            const uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);
+            z1 = bfi_op(0x0F0F0F0Fu, z, p1);  // windows 0-3 computed, 4-7 the pattern
+        } else {
+            z1 = __builtin_amdgcn_perm(p1, m_prev, 0x07020500u);  // [A oct 0, A oct 1 (pattern), B oct 0, B oct 1]
+        }
+        store_word<GSC>(dchunk, gvo, gbase, 1, z1);
+        store_word<GSC>(dchunk, gvo, gbase, 2, p2);
     };
     if constexpr (SPLIT) {
         for (int t0 = 0; t0 < tacs; t0 += kChunk) {
             prio(t0);
-            run_chunk(t0, std::true_type{});  // (frame B's padding may start in any chunk)
+            run_chunk(t0, std::true_type{}, std::false_type{});  // (frame B's padding may start in any chunk)
             if (t0 == warm - kChunk) msave = M;
         }
     } else {
@@ -1082,14 +1162,29 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         int t0 = tbeg;
         for (; t0 < tstage; t0 += kChunk) {
             prio(t0);
-            run_chunk(t0, std::false_type{});
+            run_chunk(t0, std::false_type{}, std::false_type{});
         }
         if (t0 == tstage) {
             prio(t0);
-            run_chunk(t0, std::true_type{});
+            run_chunk(t0, std::true_type{}, std::false_type{});
             t0 += kChunk;
         }
-        if (t0 < tacs) run_chunk(t0, std::false_type{});
+        if (t0 < tacs) {
+            // frames (not streams) whose last chunk holds at most 24 real steps run only its first
+            // 24 (4 groups) and write the rest of its survivor words as patterns (pad_words)
+            if (!STREAM && T - t0 <= 24 && !(dbg & 8192)) {  // VTB_DEBUG bit 13: full last chunk (measurement)
+                ng_last = 4;
+                run_chunk(t0, std::false_type{}, std::true_type{});
+                if constexpr (GS) {
+                    if (t0 < tg) pad_words(t0, std::true_type{});
+                    else pad_words(t0, std::false_type{});
+                } else {
+                    pad_words(t0, std::false_type{});
+                }
+            } else {
+                run_chunk(t0, std::false_type{}, std::false_type{});
+            }
+        }
     }
     __builtin_amdgcn_s_setprio(0);
     if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // survivor words written

@@ -38,6 +38,10 @@ for v in "$@"; do
     swz) build swz -DVTB_EXP_SWZ=2 ;;
     rn16) build rn16 -DVTB_EXP_RN=16 ;;
     nostage_noword) build nostage_noword -DVTB_EXP_NO_STAGE -DVTB_EXP_NO_WORD ;;
+    e32) build e32 -DVTB_EXP_E32 ;;
+    sgmask) build sgmask -DVTB_EXP_SGMASK ;;
+    e32sg) build e32sg -DVTB_EXP_E32 -DVTB_EXP_SGMASK ;;
+    b128) build b128 -DVTB_EXP_B128 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
