@@ -180,14 +180,16 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
         a.ws = p->ws;
         return true;
     };
-    // Longer K=7 soft frames (the LDS variant would hold the CU below 8 waves, e.g. config C3):
-    // one frame per wave as two halves with LDS survivors, persistent (launch_k7_split_loop),
-    // when the halves fit 8 waves per CU.  Measured on C3 shapes: soft 1.085
-    // vs 1.136 ms at SNR -5 dB (2.3 % of the frames re-decoded from the list), hard 0.887 vs
-    // 0.827 ms at p = 0.056 (9.6 % re-decoded; hard keeps the global variant).  VTB_KERNEL=k7s
-    // prefers it wherever it applies, hard input included; VTB_DEBUG bit 12 (measurement
-    // only): never.
-    const bool want_split = k7s || (any && !k7_in_lds && a.soft);
+    // Longer K=7 frames (the LDS variant would hold the CU below 8 waves, e.g. config C3): one
+    // frame per wave as two halves with LDS survivors, persistent (launch_k7_split_loop), when
+    // the halves fit 8 waves per CU.  Halves whose metrics disagree at the seam are fixed up in
+    // the wave (k7_pair); only frames the fix-up cannot settle go to the list kernel.  Measured
+    // on C3 shapes (round 3, DESIGN.md §4.2b, 65,536 x 2,048 bits): soft -5 dB 1.019 ms, no
+    // frame to the list (without the fix-up 1.065 ms, 1,528 frames listed); hard p = 0.056
+    // 0.808 ms against 0.805 for the global-survivor variant, whose survivor words leave the CU
+    // (7.5x the algorithmic HBM bytes).  VTB_KERNEL=k7s forces it wherever it applies;
+    // VTB_DEBUG bit 12 (measurement only): never.
+    const bool want_split = k7s || (any && !k7_in_lds);
     if (want_split && !(vtb::debug_flags() & 4096) && vtb::k7_split_loop_supported(a)) {
         if (!workspace(vtb::k7_split_loop_workspace_bytes(a))) return VTB_ERR_NOMEM;
         e = vtb::launch_k7_split_loop(a);

@@ -127,6 +127,9 @@ int t_pad(int T) { return (T + kChunk - 1) / kChunk * kChunk; }
 // 2,000 simulated soft frames at SNR -5 dB (48: 98.2 %, and every miss costs its wave a
 // second, unsplit pass).
 constexpr int kSplitWarm = 96;
+// SPLIT fix-up: chunks frame B's half may re-run from frame A's metrics before the frame falls
+// back to its slow path (k7_pair)
+constexpr int kFix = 4;
 __host__ __device__ constexpr int split_t1(int T, int warm = kSplitWarm) {
     return ((T + warm + 1) / 2 + kChunk - 1) / kChunk * kChunk;
 }
@@ -804,8 +807,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // the staged frame input)
     const uint32_t ldsA = SEG ? uint32_t(sgp->in_lds + (SOFT ? 2 : 1) * gA) : 0u;
     const uint32_t ldsB = SEG ? uint32_t(sgp->in_lds + (SOFT ? 2 : 1) * gB) : 0u;
-    const uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA));
+    uint64_t baseA = uniform64(reinterpret_cast<uint64_t>(inA));
     uint64_t baseB = uniform64(reinterpret_cast<uint64_t>(inB));
+    // SPLIT fix-up pass (below): both halves read frame B's rows (frame A's from baseB too,
+    // clamped at B's end) and survivor words go to frame B's half only
+    bool fixp = false;
     auto load_raw = [&](int c, uint32_t& ra, uint32_t& rb) {
         const int t = c * kChunk + srow;
         const uint32_t tc = uint32_t(t < T ? t : T - 1);
@@ -835,12 +841,13 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         } else if constexpr (SPLIT) {
             constexpr uint32_t SB = SOFT ? 2 : 1;
             const uint32_t tcb = uint32_t(t < Tb ? t : Tb - 1);
+            const uint32_t tca = fixp ? tcb : tc;
             if constexpr (SOFT) {
                 asm volatile("global_load_ushort %0, %2, %4\n\tglobal_load_ushort %1, %3, %5"
-                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tc), "v"(SB * tcb), "s"(baseA), "s"(baseB));
+                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tca), "v"(SB * tcb), "s"(baseA), "s"(baseB));
             } else {
                 asm volatile("global_load_ubyte %0, %2, %4\n\tglobal_load_ubyte %1, %3, %5"
-                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tc), "v"(SB * tcb), "s"(baseA), "s"(baseB));
+                             : "=&v"(ra), "=&v"(rb) : "v"(SB * tca), "v"(SB * tcb), "s"(baseA), "s"(baseB));
             }
         } else if constexpr (SOFT) {
             asm volatile("global_load_ushort %0, %2, %3\n\tglobal_load_ushort %1, %2, %4"
@@ -973,10 +980,13 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // the slot of a four-group register ring (8 groups per chunk: no copies at the loop edge)
     uint2 buf[4][6];
     constexpr int AH = VTB_EXP_AHEAD;  // groups read ahead (2 or 3)
+    auto prime = [&]() {  // the first AH groups' table pairs of a freshly staged chunk
 #pragma unroll
-    for (int g = 0; g < AH; g++)
+        for (int g = 0; g < AH; g++)
 #pragma unroll
-        for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * ring_slot(6 * g + k));
+            for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * ring_slot(6 * g + k));
+    };
+    prime();
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
@@ -1010,6 +1020,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #endif
 #define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)
 #define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)
+// (SPLIT fix-up pass: frame B's 16-bit half of the word only, frame A's stays)
+#define VTB_STORE(GSC_, W_, z_)                                                                   \
+    {                                                                                            \
+        if (SPLIT && fixp) reinterpret_cast<uint16_t*>(dchunk + (W_) * 64)[1] = uint16_t((z_) >> 16); \
+        else store_word<GSC_>(dchunk, gvo, gbase, (W_), (z_));                                   \
+    }
 #ifdef VTB_EXP_SGMASK
 #define VTB_CLR(x) sg_and(clr_mask, (x))  // measurement: the clear mask from an SGPR, no literal
 #else
@@ -1033,7 +1049,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
                 z = bfi_op(0x0F0F0F0Fu, z, pw[2] << 4);                                          \
                 z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
-                VTB_EXP_WORD(store_word<GSC>(dchunk, gvo, gbase, ((I) >> 4), z));                 \
+                VTB_EXP_WORD(VTB_STORE(GSC, (I) >> 4, z));                                      \
             }                                                                                    \
         }                                                                                        \
         if (!SOFT && ((I) & 7) == 7) {                                                           \
@@ -1042,7 +1058,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 m_prev = M;                                                                      \
             } else {                                                                             \
                 const uint32_t z = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
-                VTB_EXP_WORD(store_word<GSC>(dchunk, gvo, gbase, ((I) >> 4), z));                 \
+                VTB_EXP_WORD(VTB_STORE(GSC, (I) >> 4, z));                                      \
             }                                                                                    \
             M = VTB_RENORM_APPLY(I) ? (VTB_CLR(M) + dd) : VTB_CLR(M);                            \
         }                                                                                        \
@@ -1086,6 +1102,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
+#undef VTB_STORE
 #undef VTB_RENORM_READ
 #undef VTB_RENORM_APPLY
 #undef VTB_RD
@@ -1150,11 +1167,17 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         store_word<GSC>(dchunk, gvo, gbase, 1, z1);
         store_word<GSC>(dchunk, gvo, gbase, 2, p2);
     };
+    // SPLIT: frame B's metrics after its steps [0, warm + 48 j), j = 1..kFix (the fix-up pass's
+    // comparison points)
+    uint32_t ck[kFix] = {};
     if constexpr (SPLIT) {
         for (int t0 = 0; t0 < tacs; t0 += kChunk) {
             prio(t0);
             run_chunk(t0, std::true_type{}, std::false_type{});  // (frame B's padding may start in any chunk)
             if (t0 == warm - kChunk) msave = M;
+#pragma unroll
+            for (int j = 0; j < kFix; j++)
+                if (t0 == warm + kChunk * j) ck[j] = M;
         }
     } else {
         // chunks in order; only the one before the last stages padding rows
@@ -1210,7 +1233,36 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         constexpr uint32_t KEEP = 0xFFFFu & ~(H::SC - 1);
         const uint32_t a = M & KEEP, b = (msave >> 16) & KEEP;
         const uint32_t a0 = __builtin_amdgcn_readfirstlane(a), b0 = __builtin_amdgcn_readfirstlane(b);
-        if (__ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) != ~0ull) {
+        bool conv = __ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) == ~0ull;
+        if (!conv && !SEG && !(dbg & 16384)) {  // VTB_DEBUG bit 14: no fix-up (measurement)
+            // Fix-up: frame B's half re-runs its steps from t1 on, now from frame A's metrics
+            // at t1 (the frame's true metrics there), writing its survivor words over B's, one
+            // chunk at a time until its metric vector equals B's own at the same step up to a
+            // constant (ck): from there on B's decisions were the frame's already.  Decisions
+            // are exact either way; only a fix-up that has not converged after kFix chunks
+            // falls back to the slow path below.
+            fixp = true;
+            const uint64_t baseA0 = baseA;
+            baseA = baseB;
+            M = (M & 0xFFFFu) * kR1;  // frame A's metrics at t1 in both halves
+            uint32_t fa_, fb_;
+            load_raw(warm / kChunk, fa_, fb_);
+            stage(warm / kChunk, fa_, fb_);
+            prime();
+#pragma unroll 1
+            for (int j = 0; j < kFix && !conv; j++) {
+                const int t0 = warm + kChunk * j;
+                if (t0 + kChunk > t1s) break;  // past frame B's run: nothing left to compare
+                run_chunk(t0, std::true_type{}, std::false_type{});
+                const uint32_t fm = (M >> 16) & KEEP, bm = (ck[j] >> 16) & KEEP;
+                const uint32_t f0 = __builtin_amdgcn_readfirstlane(fm), bm0 = __builtin_amdgcn_readfirstlane(bm);
+                conv = __ballot(((fm - f0) & 0xFFFFu) == ((bm - bm0) & 0xFFFFu)) == ~0ull;
+            }
+            fixp = false;
+            baseA = baseA0;  // (the slow path below decodes frame A's rows again)
+            __syncthreads();  // the rewritten words before the traceback reads them
+        }
+        if (!conv) {
             if constexpr (LOOP) {
                 // persistent split kernel: the list kernel decodes this frame afterwards
                 if (lane == 0) {

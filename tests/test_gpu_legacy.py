@@ -264,3 +264,38 @@ def test_rand_stream_kept_across_threads(threads, frames):
         pytest.fail(f"{exe} not built (make testprogs)")
     r = subprocess.run([exe, str(threads), str(frames)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout + r.stderr)[-2000:]
+
+
+@pytest.mark.parametrize("name", sorted(GENK_REF_PARAMS))
+def test_genk_byte_count_contract(orc, name, capfd):
+    """the k>1 drop-in's per-call byte counts ('k > 1: bytes per
+    call'): every last=false call returns 0 whatever the chunking, the last=true call returns
+    the whole frame's (segments - S) k / 8 bytes equal to the oracle's decode, and a frame whose
+    (segments - S) k is not a multiple of 8 prints a message and returns 0, writing nothing."""
+    leg = Legacy(name)
+    k, K, g = GENK_REF_PARAMS[name]
+    L = 1032 if k == 3 else 1024
+    unc, rx = genk_frames(orc, k, K, g, L, 2, 0.04, 5)
+    want = orc.genk_decode(k, K, g, rx, L)
+    rng = np.random.default_rng(k)
+    for f in range(rx.shape[0]):
+        out = np.zeros(L // 8, np.uint8)
+        pos, total = 0, 0
+        while pos < rx.shape[1]:
+            n = int(min(rng.integers(1, 300), rx.shape[1] - pos))
+            last = pos + n == rx.shape[1]
+            r = leg.call(rx[f, pos:pos + n], out, last)
+            assert r == (L // 8 if last else 0), (name, pos, n, r)
+            total += r
+            pos += n
+        assert total == L // 8 and (out == want[f]).all()
+    # a frame one info segment short of whole bytes: message, 0, nothing written
+    S = K - 1
+    bad = rx[0, : rx.shape[1] - 1]  # (segments - S) k = L - k, not a multiple of 8
+    out = np.full(L // 8, 0xA5, np.uint8)
+    capfd.readouterr()
+    assert leg.call(bad, out, True) == 0
+    assert (out == 0xA5).all()
+    assert "does not hold a whole number of bytes" in capfd.readouterr().out
+    assert leg.iteration() == 0  # reset after last
+    assert (len(bad) - S) * k % 8 != 0
