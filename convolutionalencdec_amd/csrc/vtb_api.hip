@@ -74,6 +74,7 @@ struct vtb_stream {
     void* d_ring = nullptr;       // waves x 16 * ring bytes
     int t_begin = 0;              // steps decoded in the current frame (multiple of 48)
     int carry_len = 0;            // segments received but not yet decoded (< 48)
+    bool gen = false;             // generic kernel (vtb_stream_gen.hip): K other than 7, 9; no carry
 };
 
 namespace {
@@ -806,13 +807,18 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     *sp = nullptr;
     int e = check_code(code);
     if (e != VTB_OK) return e;
-    if (code->constraint_length != 7 && code->constraint_length != 9) return VTB_ERR_UNSUPPORTED;
-    const bool k9 = code->constraint_length == 9;
+    const int K = code->constraint_length;
+    // K = 7 and K = 9: their own kernels (survivor words packed per 48-step chunk, a carry of
+    // < 48 segments between calls); every other K (and K = 7 / 9 with VTB_KERNEL=lds, for
+    // testing): the generic stream kernel, all segments of a call at once
+    const bool gen = (K != 7 && K != 9) || env_flag_is("VTB_KERNEL", "lds");
+    const bool k9 = K == 9 && !gen;
     if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
     if (streams == 0 || streams > (size_t(1) << 31)) return VTB_ERR_INVALID;
     // default window: 49,152 steps (K = 7, 768 KB per wave) / 12,288 (K = 9, 64 B per step:
-    // the same 768 KB; K = 9 survivor paths merge within a few hundred steps at useful SNR)
-    const int64_t win = window_steps <= 0 ? (k9 ? 12288 : 49152) : (int64_t(window_steps) + 47) / 48 * 48;
+    // the same 768 KB; K = 9 survivor paths merge within a few hundred steps at useful SNR);
+    // generic: 16,416 steps (8 B per step and wave for up to 64 states, 16 B at K = 8, 9)
+    const int64_t win = window_steps <= 0 ? (gen ? 16416 : k9 ? 12288 : 49152) : (int64_t(window_steps) + 47) / 48 * 48;
     if (win < 96 || win > (int64_t(1) << (k9 ? 25 : 27))) return VTB_ERR_INVALID;  // 32-bit ring offsets
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return VTB_ERR_DEVICE;
@@ -826,7 +832,24 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     s->streams = streams;
     s->ring = int(win);
     s->device = device;
+    s->gen = gen;
     edge_table(code, s->symm);
+    if (gen) {
+        const int S = K - 1;
+        const size_t gw = vtb::gen_stream_waves(S, streams);
+        const size_t sw = size_t(vtb::gen_stream_state_words(S));
+        if (hipMalloc(&s->d_state, gw * sw * 4) != hipSuccess ||
+            hipMalloc(&s->d_ring, gw * vtb::gen_stream_ring_bytes_per_step(S) * size_t(s->ring)) != hipSuccess) {
+            vtb_stream_destroy(s);
+            return VTB_ERR_NOMEM;
+        }
+        if (hipMemset(s->d_state, 0, gw * sw * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            vtb_stream_destroy(s);
+            return VTB_ERR_DEVICE;
+        }
+        *sp = s;
+        return VTB_OK;
+    }
     const size_t waves = (streams + 1) / 2;
     const size_t sw = k9 ? vtb::kStreamStateWords9 : vtb::kStreamStateWords, step_bytes = k9 ? 64 : 16;
     if (hipMalloc(&s->d_state, waves * sw * 4) != hipSuccess ||
@@ -864,6 +887,42 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
     if (segments > 0 && in_stride < size_t(segments) * sb) return VTB_ERR_INVALID;
     if (out_stride < vtb_stream_out_bytes(s)) return VTB_ERR_INVALID;
     if (segments > s->ring - 48) return VTB_ERR_INVALID;
+    if (s->gen) {
+        // generic kernel: every segment of the call at once, no carry
+        const int64_t T = int64_t(s->t_begin) + segments;
+        if (T > int64_t(1) << 30) return VTB_ERR_UNSUPPORTED;
+        if (last && T < s->code.constraint_length) return VTB_ERR_INVALID;  // a frame needs L >= 1
+        DeviceGuard g(s->device);
+        if (!g.ok) return VTB_ERR_DEVICE;
+        hipStream_t hs = static_cast<hipStream_t>(stream);
+        if (!last && segments == 0) {
+            if (hipMemsetAsync(d_out_bits, 0, s->streams * sizeof(int32_t), hs) != hipSuccess) return VTB_ERR_DEVICE;
+            return VTB_OK;
+        }
+        vtb::Launch a;
+        a.S = s->code.constraint_length - 1;
+        a.soft = sb == 2;
+        a.T = int(T);
+        a.L = int(T) - a.S;
+        a.in = d_in;
+        a.in_stride = in_stride;
+        a.out = d_out;
+        a.out_stride = out_stride;
+        a.frames = s->streams;
+        a.stream = hs;
+        a.ws = s->d_ring;
+        std::memcpy(a.symm, s->symm, sizeof(a.symm));
+        vtb::StreamArgs sa;
+        sa.state = s->d_state;
+        sa.t_begin = s->t_begin;
+        sa.t_end = int(T);
+        sa.last = last ? 1 : 0;
+        sa.ring = s->ring;
+        sa.out_bits = d_out_bits;
+        if (vtb::launch_gen_stream(a, sa) != hipSuccess) return VTB_ERR_DEVICE;
+        s->t_begin = last ? 0 : int(T);
+        return VTB_OK;
+    }
     const int rows = s->carry_len + segments;  // < ring
     const int64_t T = int64_t(s->t_begin) + rows;
     if (T > int64_t(1) << 30) return VTB_ERR_UNSUPPORTED;

@@ -125,6 +125,16 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s);
 constexpr int kStreamStateWords9 = 260;  // per wave: M[4][64], e[2], flags, pad
 hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s);
 
+// Streaming decode for every K (vtb_stream_gen.hip): the generic trellis layout of the LDS
+// path (F = 64 / min(2^S, 64) streams per wave), survivor ring Launch::ws of
+// gen_stream_ring_bytes_per_step(S) bytes per step and wave, per-wave state StreamArgs::state
+// of gen_stream_state_words(S) int32 words (metrics [R][64], emitted step [64 R + f], lost flag
+// [64 R + 32 + f]).  No carry: each call runs all its segments.
+__host__ __device__ constexpr int gen_stream_state_words(int S) { return 64 * ((1 << S) < 64 ? 1 : (1 << S) / 64) + 64; }
+size_t gen_stream_waves(int S, size_t streams);
+size_t gen_stream_ring_bytes_per_step(int S);
+hipError_t launch_gen_stream(const Launch& a, const StreamArgs& s);
+
 // K=9 single-frame latency path (k9_seg_kernel): the frame as segments over `wgs` workgroups
 // of `waves` waves, input staged through LDS, survivors and metrics in a workspace (whose
 // first word, an arrival counter, must be zero before the first launch), *done as for K=7.

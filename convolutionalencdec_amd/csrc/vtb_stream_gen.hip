@@ -1,0 +1,275 @@
+// Streaming decode (vtb_stream_*) for every constraint length the K=7 / K=9
+// stream kernels do not cover (K = 3..9), on the generic trellis layout of vtb_lds_path.hip.
+//
+// The reference's chunked protocol (viterbiDecoderHardButterflyk1 with last=false, then
+// last=true, src/viterbiDecoderButterflyk1.c:82-263) keeps metrics and survivors between
+// calls and traces back only at `last`; its windowed traceback is a TODO (:195, 199).  Here a
+// batch of streams advances in lockstep, one launch per call, and every stream emits the bits
+// that became final during the call:
+//   * ACS over the call's segments (all of them: no 48-step granularity, so no carry), one
+//     wave per F = 64 / G streams, state s of stream fi in lane fi*G + s % G, register s / G
+//     (vtb_lds_path.hip's layout and arithmetic: centred int32 metrics, strict '>' ties to the
+//     lower predecessor, :129-130), decisions as one ballot word per register per step into a
+//     per-wave survivor ring in global memory (step t at t mod W);
+//   * not last: walks from all N states at the call's end go back one step at a time until
+//     they stand on one state (step m); every survivor path passes through it, so no later
+//     input can change the bits below m: they equal the whole-frame decode's and are emitted
+//     by the verified block-parallel traceback of vtb_lds_path.hip over [e, hi), hi = m rounded
+//     down to a whole number of bytes past e and at most the call's end minus K-1 (so the
+//     terminating zero tail is never emitted early);
+//   * last: the terminated traceback from state 0 at T emits [e, T - K + 1).
+// Metrics are renormalised against state 0 at the end of every call (their spread is bounded),
+// so a stream may run for any number of steps (< 2^30).  A stream that goes W steps without a
+// merge has lost survivors it still needs: it reports -1 until `last`, then restarts.
+
+#include "vtb_internal.h"
+
+namespace vtb {
+namespace {
+
+template <int S>
+struct SGeo {
+    static constexpr int N = 1 << S;
+    static constexpr int G = N < 64 ? N : 64;  // lanes per stream
+    static constexpr int R = N / G;            // states per lane
+    static constexpr int F = 64 / G;           // streams per wave
+};
+
+constexpr int kStage = 64;  // steps of input staged into LDS per round
+
+__device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
+
+template <int S, bool SOFT>
+__global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                        uint8_t* __restrict__ out, size_t out_stride, size_t streams,
+                                                        Launch table, StreamArgs sa, uint64_t* __restrict__ ring,
+                                                        int32_t* __restrict__ state) {
+    using Gm = SGeo<S>;
+    constexpr int N = Gm::N, G = Gm::G, R = Gm::R, F = Gm::F;
+    constexpr int Q = SOFT ? 255 : 1;
+    constexpr int INIT = int(uint8_t(N + 1)) * Q;  // (uint8_t)(NUM_STATES+1), reference :62
+    constexpr int SB = SOFT ? 2 : 1;
+    extern __shared__ uint8_t sm[];  // F x kStage x SB staged input bytes
+    const int lane = threadIdx.x, fi = lane / G, lam = lane % G;
+    const size_t f0 = size_t(blockIdx.x) * F, myf = f0 + fi;
+    const bool real = myf < streams;
+    const int W = sa.ring;
+    uint64_t* rg = ring + size_t(blockIdx.x) * size_t(W) * R;
+    int32_t* st = state + size_t(blockIdx.x) * gen_stream_state_words(S);
+    const int C = sa.t_end - sa.t_begin;  // steps of this call
+
+    // branch-metric coefficients of the lane's destinations (vtb_lds_path.hip)
+    int sig[R], kap[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int d = r * G + lam, c = table.symm[d >> 1], sb = (d & 1) ? -1 : 1;
+        const int s0 = ((c & 1) ? -1 : 1) * sb, s1 = ((c & 2) ? -1 : 1) * sb;
+        sig[r] = (s0 & 0xffff) | (s1 << 16);
+        kap[r] = (((c & 1) + ((c >> 1) & 1)) - 1) * Q * sb;
+    }
+    int m[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) m[r] = sa.t_begin == 0 ? ((r * G + lam == 0) ? 0 : INIT) : st[r * 64 + lane];
+
+    // ---- ACS over the call's steps ----
+    typedef short short2_t __attribute__((ext_vector_type(2)));
+    for (int c0 = 0; c0 < C; c0 += kStage) {
+        const int n = C - c0 < kStage ? C - c0 : kStage;
+        __syncthreads();
+        for (int idx = lane; idx < F * n * SB; idx += 64) {
+            const int f = idx / (n * SB), o = idx - f * (n * SB);
+            sm[f * kStage * SB + o] = f0 + f < streams ? in[(f0 + f) * in_stride + size_t(c0) * SB + o] : 0;
+        }
+        __syncthreads();
+        const uint8_t* my = sm + fi * kStage * SB;
+        for (int i = 0; i < n; i++) {
+            int qp;
+            if constexpr (SOFT) {
+                qp = int(my[2 * i]) | (int(my[2 * i + 1]) << 16);
+            } else {
+                const int c = my[i];
+                qp = (c & 1) | (((c >> 1) & 1) << 16);
+            }
+            int nm[R];
+            uint64_t bal[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int l0 = fi * G + (r & 1) * (G / 2) + (lam >> 1);
+                int a0, a1;
+                if constexpr (R == 1) {
+                    a0 = bperm(m[0], l0);
+                    a1 = bperm(m[0], l0 + G / 2);
+                } else {
+                    a0 = bperm(m[r >> 1], l0);
+                    a1 = bperm(m[(r >> 1) + R / 2], l0);
+                }
+                const int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, sig[r]), __builtin_bit_cast(short2_t, qp),
+                                                      kap[r], false);
+                const int x0 = a0 + mu, x1 = a1 - mu;
+                const bool dd = x0 > x1;  // strict: ties keep the lower predecessor
+                nm[r] = dd ? x1 : x0;
+                bal[r] = __ballot(dd);
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) m[r] = nm[r];
+            if (lane == 0) {
+                const size_t slot = size_t((sa.t_begin + c0 + i) % W) * R;
+#pragma unroll
+                for (int r = 0; r < R; r++) rg[slot + r] = bal[r];
+            }
+        }
+    }
+    // renormalise against state 0 of the lane's stream, keep the metrics for the next call
+    const int ref = __shfl(m[0], fi * G);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        m[r] -= ref;
+        if (!sa.last) st[r * 64 + lane] = m[r];
+    }
+    __threadfence_block();  // the ring words of this call before any walk reads them
+    __syncthreads();
+
+    auto pred = [&](unsigned s, int t) -> unsigned {
+        const uint64_t w = rg[size_t(t % W) * R + (s / G)];
+        return (s >> 1) | (unsigned((w >> (fi * G + (s % G))) & 1u) << (S - 1));
+    };
+    const int e0 = st[64 * R + fi];
+    const int flags = st[64 * R + 32 + fi];
+    const bool lost = flags != 0 || sa.t_end - e0 > W;
+    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << G) - 1)) << (fi * G);
+
+    int hi = e0;
+    unsigned kloc = 0;
+    if (sa.last) {
+        hi = sa.t_end;
+    } else {
+        // merge test: walkers from every state at the call's end, one step back at a time,
+        // until all walkers of a stream stand on one state (its last S steps excluded: the
+        // zero tail of a frame that ends in the next call must not be emitted early)
+        const int cap = sa.t_end - S;
+        unsigned wk[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) wk[r] = unsigned(r * G + lam);
+        bool walking = real && !lost && cap > e0;
+        int t = sa.t_end;
+        while (__ballot(walking) != 0) {
+            if (walking) {
+                t--;
+#pragma unroll
+                for (int r = 0; r < R; r++) wk[r] = pred(wk[r], t);
+            }
+            const unsigned r0 = unsigned(__shfl(int(wk[0]), fi * G));
+            bool same = true;
+#pragma unroll
+            for (int r = 0; r < R; r++) same = same && wk[r] == r0;
+            const bool merged = (__ballot(same) & fmask) == fmask;
+            if (walking && merged) {
+                // every survivor path passes through state r0 at step t: bits below it are final;
+                // walk on to a whole number of bytes past e0 (and below the tail cap)
+                const int lim = t < cap ? t : cap;
+                const int h = e0 + (lim - e0) / 8 * 8;
+                unsigned s0 = r0;
+                for (int u = t - 1; u >= h; u--) s0 = pred(s0, u);
+                hi = h, kloc = s0;
+                walking = false;
+            }
+            if (walking && t <= e0) walking = false;
+        }
+    }
+    // emission of [e0, hi): the verified block-parallel traceback over the stream's G lanes
+    // (every lane runs the loops, so the cross-lane checks see the whole wave)
+    const int emit_end = sa.last ? sa.t_end - S : hi;  // bits past the terminated tail are not output
+    const bool emits = real && !lost && hi > e0;
+    {
+        constexpr int kWarm = 8 * S + 48;
+        const int n = hi - e0;
+        const int tbb = emits ? ((n + G - 1) / G + 7) / 8 * 8 : 8;
+        const int lo = e0 + lam * tbb, top = lo + tbb < hi ? lo + tbb : hi;
+        const bool active = emits && lo < hi;
+        const int start = top + kWarm < hi ? top + kWarm : hi;
+        unsigned s = start == hi ? kloc : 0u;
+        for (int t = start - 1; active && t >= top; t--) s = pred(s, t);
+        unsigned s_top = s;
+        for (int t = top - 1; active && t >= lo; t--) s = pred(s, t);
+        unsigned fin = s;
+        bool fixed = !active || start == hi;
+        for (int round = 0; round <= G; round++) {
+            const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
+            const bool ok = fixed || s_top == sf;
+            const uint64_t bad = ~__ballot(ok);
+            if (bad == 0) break;
+            const uint64_t badf = (bad & fmask) >> (fi * G);  // this stream's failed blocks
+            if (!ok && (badf >> (lam + 1)) == 0) {
+                s = s_top = sf;
+                for (int t = top - 1; t >= lo; t--) s = pred(s, t);
+                fin = s;
+                fixed = true;
+            }
+        }
+        if (active) {
+            uint8_t* o = out + myf * out_stride;
+            unsigned byte = 0;
+            s = s_top;
+            for (int t = top - 1; t >= lo; t--) {
+                byte = ((byte >> 1) | ((s & 1u) << 7)) & 0xffu;
+                const int rel = t - e0;
+                if ((rel & 7) == 0 && t < emit_end) {
+                    const int keep = emit_end - t;  // bits of this byte still inside the output
+                    o[rel >> 3] = uint8_t(keep >= 8 ? byte : byte & (0xffu << (8 - keep)));
+                }
+                s = pred(s, t);
+            }
+        }
+    }
+    if (real && lam == 0) {
+        sa.out_bits[myf] = lost ? -1 : (sa.last ? emit_end - e0 : hi - e0);
+        st[64 * R + fi] = sa.last ? 0 : (lost ? e0 : hi);
+        st[64 * R + 32 + fi] = sa.last ? 0 : (lost ? 1 : 0);
+    }
+}
+
+template <int S, bool SOFT>
+hipError_t launch_typed(const Launch& a, const StreamArgs& s) {
+    using Gm = SGeo<S>;
+    const size_t waves = (a.frames + Gm::F - 1) / Gm::F;
+    const size_t lds = size_t(Gm::F) * kStage * (SOFT ? 2 : 1);
+    hipLaunchKernelGGL((gen_stream_kernel<S, SOFT>), dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride,
+                       a.out, a.out_stride, a.frames, a, s, static_cast<uint64_t*>(a.ws),
+                       reinterpret_cast<int32_t*>(s.state));
+    return hipGetLastError();
+}
+
+template <bool SOFT>
+hipError_t launch_soft(const Launch& a, const StreamArgs& s) {
+    switch (a.S) {
+        case 2: return launch_typed<2, SOFT>(a, s);
+        case 3: return launch_typed<3, SOFT>(a, s);
+        case 4: return launch_typed<4, SOFT>(a, s);
+        case 5: return launch_typed<5, SOFT>(a, s);
+        case 6: return launch_typed<6, SOFT>(a, s);
+        case 7: return launch_typed<7, SOFT>(a, s);
+        case 8: return launch_typed<8, SOFT>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+size_t gen_stream_waves(int S, size_t streams) {
+    const int N = 1 << S, G = N < 64 ? N : 64, F = 64 / G;
+    return (streams + F - 1) / F;
+}
+
+size_t gen_stream_ring_bytes_per_step(int S) {
+    const int N = 1 << S, G = N < 64 ? N : 64;
+    return size_t(N / G) * 8;
+}
+
+hipError_t launch_gen_stream(const Launch& a, const StreamArgs& s) {
+    if (a.frames == 0) return hipSuccess;
+    if (!a.ws || !s.state || !s.out_bits || s.ring < 48 || a.S < 2 || a.S > kMaxS) return hipErrorInvalidValue;
+    note_kernel("gen_stream");
+    return a.soft ? launch_soft<true>(a, s) : launch_soft<false>(a, s);
+}
+
+}  // namespace vtb

@@ -179,7 +179,7 @@ class ViterbiDecoder:
 
 
 class ViterbiStream:
-    """Streaming decoder over the C ABI (vtb_stream_*; K=7): `streams` independent streams
+    """Streaming decoder over the C ABI (vtb_stream_*; any K): `streams` independent streams
     advancing in lockstep on one device.  push(chunk, last) feeds `segments` more coded
     segments per stream (torch uint8 tensor on the device, [streams, segments] hard or
     [streams, segments, 2] / [streams, 2*segments] soft) and returns (bytes, nbits): row i of

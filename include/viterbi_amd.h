@@ -193,9 +193,11 @@ int vtb_device_count(void);
  * device memory.  Output bits wait until the paths merge; should a stream go window_steps
  * steps without a merge (pure-noise input), its frame is lost: d_out_bits reports -1 for it
  * until the call with last != 0, after which it restarts cleanly.
- * K = 7 and K = 9 (VTB_ERR_UNSUPPORTED otherwise); hard or soft input as for plans.  The ring
- * holds 16 (K = 7) or 64 (K = 9) bytes per step per pair of streams; window_steps <= 0 selects
- * 49152 steps at K = 7 and 12288 at K = 9. */
+ * Every K in VTB_MIN_K..VTB_MAX_K; hard or soft input as for plans.  K = 7 and K = 9 run their
+ * own kernels (the ring holds 16 or 64 bytes per step per pair of streams; window_steps <= 0
+ * selects 49152 and 12288 steps); every other K the generic kernel (csrc/vtb_stream_gen.hip:
+ * 64 / min(2^(K-1), 64) streams per wave, 8 bytes per step and wave up to K = 7, 16 at K = 8;
+ * window_steps <= 0 selects 16416 steps). */
 typedef struct vtb_stream vtb_stream_t;
 
 int vtb_stream_create(vtb_stream_t** s, const vtb_code_t* code, vtb_input_t input, size_t streams,

@@ -183,7 +183,10 @@ def test_stream_api_errors():
     c = CODE._c()
     h = ctypes.c_void_p()
     k5 = ConvCode(5, CODES[5])._c()
-    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(k5), 0, 4, 0, 0) == native.VTB_ERR_UNSUPPORTED
+    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(k5), 0, 4, 0, 0) == native.VTB_OK  # generic kernel
+    L.vtb_stream_destroy(h)
+    bad = ConvCode(11, (0o2011, 0o3777))._c()  # past VTB_MAX_K
+    assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(bad), 0, 4, 0, 0) == native.VTB_ERR_UNSUPPORTED
     assert L.vtb_stream_create(ctypes.byref(h), ctypes.byref(c), 0, 0, 0, 0) == native.VTB_ERR_INVALID
     vs = ViterbiStream(CODE, streams=2, window_steps=96)
     x = torch.zeros((2, 100), dtype=torch.uint8, device="cuda")

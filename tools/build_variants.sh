@@ -7,7 +7,7 @@ build() {
   name=$1; shift
   d=convolutionalencdec_amd/lib/exp/$name; mkdir -p $d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -I$CS "$@" \
-      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_k9.hip $CS/vtb_gen.hip $CS/vtb_genk.hip $CS/vtb_legacy.hip
+      -o $d/libviterbi_amd.so $CS/vtb_api.hip $CS/vtb_lds_path.hip $CS/vtb_k7_lds.hip $CS/vtb_k9.hip $CS/vtb_gen.hip $CS/vtb_genk.hip $CS/vtb_legacy.hip $CS/vtb_stream_gen.hip
 }
 for v in "$@"; do
   case $v in
