@@ -36,7 +36,10 @@ uint32_t gen_rev(uint64_t v, int bits) {  // convEncode.c:163-174
 
 struct GenArgs {
     int k, S, n, N, T, L, R;
+    int ptr_bytes;   // survivor-pointer bytes per frame (gen_ptr_bytes)
     int u8;          // VTB_GENK_K1_REFERENCE_U8: the reference's k=1 butterfly arithmetic (below)
+    int warm;        // traceback warm-up steps per block (any value is exact: the walk is verified)
+    int dbg;         // $VTB_DEBUG (measurement only): bit 0 skips the traceback, bit 1 the ACS
     uint32_t rg[8];  // generators bit-reversed over k*K bits (convEncode.c:163-174)
 };
 
@@ -51,33 +54,79 @@ struct GenLayout {  // LDS byte offsets
     size_t tab, met, inb, outb, dec, total;
 };
 
-GenLayout gen_layout(int N, int E, int T, int L, int R, int k, bool gdec) {
+// Survivor pointers (round 3).  Every state carries V = (m << 12) | (e << 8) | ptr: m its path
+// metric (20 bits: at most n T < 2^18), e its own top k bits -- the edge index under which all
+// its successors see it (src = d / 2^k + e 2^((S-1)k)) -- and ptr the state its survivor path
+// passed through at the last boundary.  A candidate is then V_src + (bm << 12): one min over
+// the 2^k candidates gives the metric, the first minimum (lowest e among equal metrics, the
+// reference's argmin: e sits below the metric) and the survivor's pointer in one value, so the
+// per-step decisions are never stored.  Boundaries are the steps t = t_b (mod S), t_b = (T-1)
+// mod S: there each state's ptr (8 bits) is written out and reset to the state itself.  A
+// state's S steps of inputs are its own bits, so the traceback jumps S steps per read and
+// emits the state at each boundary as the kS output bits of that window.
+constexpr int kMetShift = 12;
+
+// Boundaries of a frame of T steps (S steps apart, the last at step T-1) and their pointer bytes.
+__host__ __device__ constexpr int gen_boundaries(int T, int S) { return (T - 1) / S + 1; }
+size_t gen_ptr_bytes(int T, int S, int N) { return size_t(gen_boundaries(T, S)) * size_t(N < 4 ? 4 : N); }
+
+GenLayout gen_layout(int N, int E, int T, int L, int S, bool gdec) {
     GenLayout l;
-    l.dec = 0;                                             // T * R * k u64 words (in LDS unless gdec)
-    l.met = l.dec + (gdec ? 0 : 8 * size_t(T) * R * k);   // 2 * N int32
-    l.tab = l.met + 8 * size_t(N);                   // N * E bytes
-    l.inb = (l.tab + size_t(N) * E + 15) & ~size_t(15);  // T bytes
-    l.outb = (l.inb + size_t(T) + 15) & ~size_t(15);     // ceil(L / 8) bytes
+    l.dec = 0;                                                         // pointer bytes (in LDS unless gdec)
+    l.met = (l.dec + (gdec ? 0 : gen_ptr_bytes(T, S, N)) + 15) & ~size_t(15);  // 2 * N uint32
+    l.tab = l.met + 8 * size_t(N);                                     // N * E bytes
+    l.inb = (l.tab + size_t(N) * E + 15) & ~size_t(15);               // T + 1 bytes
+    l.outb = (l.inb + size_t(T) + 1 + 15) & ~size_t(15);              // ceil(L / 8) bytes
     l.total = (l.outb + size_t((L + 7) / 8) + 15) & ~size_t(15);
     return l;
 }
 
-// N <= 64 states: one state per lane, its metric in a register, the 2^k predecessors gathered
+// The state's constant low 12 bits: e << 8 | (d & 0xFF) (the pointer reset value).
+__device__ __forceinline__ uint32_t own_tag(int d, int kS, int KB) {
+    return (uint32_t(d >> (kS - KB)) << 8) | uint32_t(d & 0xFF);
+}
+
+// Branch metrics.  PK (n <= 3): the branch metrics of all 2^n labels for the step's received
+// segment rx packed 4 bits per label in one word (ptab: lane x holds the word for rx = x, read
+// back with v_readlane), so a candidate is V + (bfe(P, 4 lab, 4) << 12): two instructions per
+// edge.  Otherwise popc(lab ^ rx): three.
+template <bool PK>
+__device__ __forceinline__ uint32_t gen_cand(uint32_t v, uint32_t lab, uint32_t rx, uint32_t P) {
+    if (PK) return (__builtin_amdgcn_ubfe(P, lab, 4) << kMetShift) + v;
+    return (uint32_t(__popc(lab ^ rx)) << kMetShift) + v;
+}
+
+__device__ __forceinline__ uint32_t gen_ptab(int n, int lane) {
+    uint32_t p = 0;
+    for (int x = 0; x < (1 << n); x++) p |= uint32_t(__popc(uint32_t(x) ^ uint32_t(lane))) << (4 * x);
+    return p;
+}
+
+// The new state value: the winning candidate with its e field (and at a boundary its pointer)
+// replaced by the state's own.
+__device__ __forceinline__ uint32_t gen_next(uint32_t best, uint32_t tag, bool bnd) {
+    const uint32_t mask = bnd ? 0xFFFu : 0xF00u;
+    return (best & ~mask) | (tag & mask);
+}
+
+// N <= 64 states: one state per lane, its value in a register, the 2^k predecessors gathered
 // with ds_bpermute, the lane's 2^k edge labels (time-invariant) in registers; k is a template
-// parameter so every per-edge loop is unrolled.
+// parameter so every per-edge loop is unrolled.  Pointers: one byte per state and boundary.
 //
 // U8 (k = 1 only): the reference's k=1 butterfly arithmetic (viterbiDecoderButterflyk1.c:101-183)
 // -- the upper predecessor's branch metric is n minus the lower's, whatever the generators
 // (:104-107), sums wrap mod 256 (uint8 METRIC_TYPE), the strict '>' keeps the lower predecessor
 // on ties (:129-130), and when the counter reaches 120 the minimum is subtracted (:159-183) --
 // so that codes whose uint8 sums can wrap (n >= 4) decode exactly as the reference does.
-template <int KB, bool U8 = false>
-__device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
-                                       int32_t* met, uint64_t* dec, int lane) {
+template <int KB, bool U8 = false, bool PK = false>
+__device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t* inb, uint32_t nmask,
+                                       const uint8_t* tab, const int32_t* met, uint8_t* ptrs, int lane) {
     constexpr int E = 1 << KB;
+    const int kS = KB * S;
     const int d = lane;
     const bool live = d < N;
-    int32_t m = live ? met[d] : 0;
+    const uint32_t tag = live ? own_tag(d, kS, KB) : 0u;
+    uint32_t v = live ? (uint32_t(met[d]) << kMetShift) | tag : 0u;
     uint32_t lab[E];
     int srcl[E];
 #pragma unroll
@@ -88,83 +137,103 @@ __device__ __forceinline__ void acs_r1(int N, int kS, int T, const uint8_t* inb,
             lab[e] = live ? uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u) : 0u;
         else
             lab[e] = live ? uint32_t(tab[(src << KB) | (d & (E - 1))]) : 0u;
+        if (PK) lab[e] *= 4;  // bit offset of the label's field in the packed word
     }
+    const uint32_t ptab = PK ? gen_ptab(n, lane) : 0u;
     uint32_t renorm = 0;
+    int cnt = S - 1 - (T - 1) % S, bi = 0;  // steps into the current window, boundary index
     for (int t = 0; t < T; t++) {
         const uint32_t rx = inb[t] & nmask;
+        const uint32_t P = PK ? __builtin_amdgcn_readlane(ptab, __builtin_amdgcn_readfirstlane(rx)) : 0u;
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
         for (int e = 0; e < E; e++) {
-            uint32_t pm = uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], m)) + uint32_t(__popc(lab[e] ^ rx));
-            if (U8) pm &= 0xFFu;
-            best = min(best, (pm << 4) | uint32_t(e));
+            uint32_t c = gen_cand<PK>(uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], int(v))), lab[e], rx, P);
+            if (U8) c &= 0xFFFFFu;  // (pm + bm) mod 256
+            best = min(best, c);
         }
-        m = int32_t(best >> 4);
+        const bool bnd = cnt == S - 1;
+        cnt = bnd ? 0 : cnt + 1;
+        if (bnd) {
+            if (live) ptrs[size_t(bi) * size_t(N < 4 ? 4 : N) + d] = uint8_t(best);
+            bi++;
+        }
+        v = gen_next(best, tag, bnd);
         if (U8) {
             if (renorm >= 120) {
-                m -= int32_t(wave_min(live ? uint32_t(m) : 0xFFu));
+                v -= wave_min(live ? v : 0xFFFFFFFFu) & ~0xFFFu;
                 renorm = 0;
             } else {
                 renorm++;
             }
-        }
-        const int be = int(best & 15u);
-#pragma unroll
-        for (int j = 0; j < KB; j++) {
-            const uint64_t w = __ballot(live && ((be >> j) & 1));
-            if (lane == j) dec[size_t(t) * KB + j] = w;
         }
     }
 }
 
 // N = 256 states (k * S = 8: k = 1, 2 or 4), four states per lane: d = 64 r + lane.  The
 // 4 * 2^k edge labels of a lane's states are time-invariant and sit in registers (compile-time
-// indices: k is a template parameter), the previous metrics in LDS (double-buffered).
-template <int KB, bool U8 = false>
-__device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
-                                       int32_t* met, uint64_t* dec, int lane) {
-    constexpr int E = 1 << KB, kS = 8, N = 256;
-    uint32_t lab[4][E];
+// indices: k is a template parameter), the previous values in LDS (double-buffered; the 2^k
+// predecessors of a lane's state r are one base address apart by compile-time offsets).
+// Pointers: a dword per lane and boundary, byte r = state 64 r + lane (gen_ptr below).
+template <int KB, bool U8 = false, bool PK = false>
+__device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
+                                       uint32_t* met, uint32_t* ptr32, int lane) {
+    constexpr int E = 1 << KB, kS = 8, N = 256, S = 8 / KB;
+    uint32_t lab[4][E], tag[4];
     int sbase[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int d = r * 64 + lane;
         sbase[r] = d >> KB;
+        tag[r] = own_tag(d, kS, KB);
+        met[r * 64 + lane] = (met[r * 64 + lane] << kMetShift) | tag[r];
 #pragma unroll
         for (int e = 0; e < E; e++) {
             if (U8)  // the butterfly identity of acs_r1 U8
                 lab[r][e] = uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u);
             else
                 lab[r][e] = uint32_t(tab[(((d >> KB) | (e << (kS - KB))) << KB) | (d & (E - 1))]);
+            if (PK) lab[r][e] *= 4;
         }
     }
+    const uint32_t ptab = PK ? gen_ptab(n, lane) : 0u;
     int cur = 0;
     uint32_t renorm = 0;
+    int cnt = S - 1 - (T - 1) % S, bi = 0;
+    // (PK: the next step's packed word is fetched a step ahead, off the metric chain; inb[T] is
+    // inside the LDS layout, its value unused)
+    uint32_t Pn = PK ? __builtin_amdgcn_readlane(ptab, __builtin_amdgcn_readfirstlane(inb[0] & nmask)) : 0u;
     for (int t = 0; t < T; t++) {
         const uint32_t rx = inb[t] & nmask;
-        const int32_t* mc = met + cur * N;
-        int32_t* mn = met + (cur ^ 1) * N;
+        const uint32_t P = Pn;
+        if (PK) Pn = __builtin_amdgcn_readlane(ptab, __builtin_amdgcn_readfirstlane(inb[t + 1] & nmask));
+        const uint32_t* mc = met + cur * N;
+        uint32_t* mn = met + (cur ^ 1) * N;
+        const bool bnd = cnt == S - 1;
+        cnt = bnd ? 0 : cnt + 1;
         uint32_t nm[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
+            const uint32_t* ps = mc + sbase[r];  // predecessor e at ps[e << (kS - KB)]
             uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
             for (int e = 0; e < E; e++) {
-                uint32_t pm = uint32_t(mc[sbase[r] | (e << (kS - KB))]) + uint32_t(__popc(lab[r][e] ^ rx));
-                if (U8) pm &= 0xFFu;
-                best = min(best, (pm << 4) | uint32_t(e));
+                uint32_t c = gen_cand<PK>(ps[e << (kS - KB)], lab[r][e], rx, P);
+                if (U8) c &= 0xFFFFFu;
+                best = min(best, c);
             }
-            nm[r] = best >> 4;
-            const int be = int(best & 15u);
-#pragma unroll
-            for (int j = 0; j < KB; j++) {
-                const uint64_t w = __ballot((be >> j) & 1);
-                if (lane == j) dec[(size_t(t) * 4 + r) * KB + j] = w;
-            }
+            nm[r] = best;
         }
+        if (bnd) {
+            ptr32[size_t(bi) * 64 + lane] = __builtin_amdgcn_perm(nm[1], nm[0], 0x0c0c0400u) |
+                                            __builtin_amdgcn_perm(nm[3], nm[2], 0x04000c0cu);
+            bi++;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) nm[r] = gen_next(nm[r], tag[r], bnd);
         if (U8) {
             if (renorm >= 120) {
-                const uint32_t mn4 = wave_min(min(min(nm[0], nm[1]), min(nm[2], nm[3])));
+                const uint32_t mn4 = wave_min(min(min(nm[0], nm[1]), min(nm[2], nm[3]))) & ~0xFFFu;
 #pragma unroll
                 for (int r = 0; r < 4; r++) nm[r] -= mn4;
                 renorm = 0;
@@ -173,93 +242,114 @@ __device__ __forceinline__ void acs_r4(const GenArgs& a, int T, const uint8_t* i
             }
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++) mn[r * 64 + lane] = int32_t(nm[r]);
+        for (int r = 0; r < 4; r++) mn[r * 64 + lane] = nm[r];
         cur ^= 1;
-        __syncthreads();
+        // one wave per workgroup: its LDS accesses complete in issue order, so the next step's
+        // reads see these writes without a workgroup barrier (a compiler fence keeps the order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
-    (void)a;
 }
 
-// GDEC: decision words in a global workspace (one slot per frame of the launch) instead of
-// LDS, for trellises whose words would hold the CU to one or two waves.
+// GDEC: pointer bytes in a global workspace (one slot per frame of the launch) instead of
+// LDS, for trellises whose pointers would hold the CU to few waves.
 template <bool GDEC>
 __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                   uint8_t* __restrict__ out, size_t out_stride, size_t frames,
-                                                  GenArgs a, GenLayout ly, uint64_t* __restrict__ ws) {
+                                                  GenArgs a, GenLayout ly, uint8_t* __restrict__ ws) {
     extern __shared__ uint64_t gsm[];
     uint8_t* sm = reinterpret_cast<uint8_t*>(gsm);
-    uint64_t* dec = GDEC ? ws + size_t(blockIdx.x) * size_t(a.T) * a.R * a.k : reinterpret_cast<uint64_t*>(sm + ly.dec);
-    int32_t* met = reinterpret_cast<int32_t*>(sm + ly.met);
+    uint8_t* ptrs = GDEC ? ws + size_t(blockIdx.x) * size_t(a.ptr_bytes) : sm + ly.dec;
+    uint32_t* met = reinterpret_cast<uint32_t*>(sm + ly.met);
     uint8_t* tab = sm + ly.tab;
     uint8_t* inb = sm + ly.inb;
     uint8_t* outb = sm + ly.outb;
     const int lane = threadIdx.x;
     const size_t f = blockIdx.x;
     if (f >= frames) return;
-    const int k = a.k, N = a.N, E = 1 << k, kS = k * a.S, T = a.T, R = a.R;
-    const uint32_t nmask = (1u << a.n) - 1u;
+    const int k = a.k, N = a.N, E = 1 << k, S = a.S, kS = k * S, T = a.T, R = a.R, n = a.n;
+    const uint32_t nmask = (1u << n) - 1u;
 
     for (int i = lane; i < N * E; i += 64) {  // edge labels, index = delay (src << k) | bits
         uint32_t o = 0;
-        for (int j = 0; j < a.n; j++) o |= (uint32_t(__popc(uint32_t(i) & a.rg[j])) & 1u) << j;
+        for (int j = 0; j < n; j++) o |= (uint32_t(__popc(uint32_t(i) & a.rg[j])) & 1u) << j;
         tab[i] = uint8_t(o);
     }
     const uint8_t* row = in + f * in_stride;
-    for (int i = lane; i < T; i += 64) inb[i] = row[i];
+    for (int i = lane; i <= T; i += 64) inb[i] = i < T ? row[i] : 0;
     for (int i = lane; i < (a.L + 7) / 8; i += 64) outb[i] = 0;
-    const int32_t init = int32_t(uint8_t(N + 1));
+    const uint32_t init = uint8_t(N + 1);
     for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
     __syncthreads();
 
-    // Candidates carry their predecessor index: cand = (pm << 4) | e, so one min gives the
-    // metric and the first minimum (lowest e among equal metrics, the reference's argmin).
-    if (R == 1) {
+    const bool pk = n <= 3;
+    if (a.dbg & 2) {
+    } else if (R == 1) {
+        const int32_t* m0 = reinterpret_cast<const int32_t*>(met);
         switch (k) {
             case 1:
                 if (a.u8)
-                    acs_r1<1, true>(N, kS, T, inb, nmask, tab, met, dec, lane);
+                    pk ? acs_r1<1, true, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+                       : acs_r1<1, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
                 else
-                    acs_r1<1>(N, kS, T, inb, nmask, tab, met, dec, lane);
+                    pk ? acs_r1<1, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+                       : acs_r1<1>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
                 break;
-            case 2: acs_r1<2>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
-            case 3: acs_r1<3>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
-            default: acs_r1<4>(N, kS, T, inb, nmask, tab, met, dec, lane); break;
+            case 2:
+                pk ? acs_r1<2, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+                   : acs_r1<2>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+                break;
+            case 3:
+                pk ? acs_r1<3, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+                   : acs_r1<3>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+                break;
+            default:
+                pk ? acs_r1<4, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+                   : acs_r1<4>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+                break;
         }
-        __syncthreads();
-    } else if (k == 1) {
-        if (a.u8)
-            acs_r4<1, true>(a, T, inb, nmask, tab, met, dec, lane);
-        else
-            acs_r4<1>(a, T, inb, nmask, tab, met, dec, lane);
-    } else if (k == 2) {
-        acs_r4<2>(a, T, inb, nmask, tab, met, dec, lane);
     } else {
-        acs_r4<4>(a, T, inb, nmask, tab, met, dec, lane);
+        uint32_t* p32 = reinterpret_cast<uint32_t*>(ptrs);
+        if (k == 1) {
+            if (a.u8)
+                pk ? acs_r4<1, true, true>(T, n, inb, nmask, tab, met, p32, lane)
+                   : acs_r4<1, true>(T, n, inb, nmask, tab, met, p32, lane);
+            else
+                pk ? acs_r4<1, false, true>(T, n, inb, nmask, tab, met, p32, lane)
+                   : acs_r4<1>(T, n, inb, nmask, tab, met, p32, lane);
+        } else if (k == 2) {
+            pk ? acs_r4<2, false, true>(T, n, inb, nmask, tab, met, p32, lane)
+               : acs_r4<2>(T, n, inb, nmask, tab, met, p32, lane);
+        } else {
+            pk ? acs_r4<4, false, true>(T, n, inb, nmask, tab, met, p32, lane)
+               : acs_r4<4>(T, n, inb, nmask, tab, met, p32, lane);
+        }
     }
+    __syncthreads();
 
-    // Traceback from state 0 (terminated frame), block-parallel and verified (the K=7
-    // kernel's scheme, vtb_k7_lds.hip): lane b walks steps [b tbb, (b+1) tbb) back from
-    // kGenWarm steps past its block's end, starting from state 0 there (exact when the walk
-    // starts at T).  A block is right if it entered on its successor's exit state and that
-    // successor is proven; failed blocks re-walk from a proven successor until all are
-    // proven.  Then every lane emits its block's bits (LDS atomic OR: blocks share bytes).
-    {
-        constexpr int kGenWarm = 96;
-        auto pred = [&](int s, int t) {
-            const uint64_t* w = dec + (size_t(t) * R + (s >> 6)) * k;
-            int e = 0;
-            for (int j = 0; j < k; j++) e |= int((w[j] >> (s & 63)) & 1u) << j;
-            return (s >> k) | (e << (kS - k));
+    // Traceback over the boundaries (i = 0 .. nb-1, boundary i at step t_b + i S, the last at
+    // T-1 where the terminated frame is in state 0), block-parallel and verified (the K=7
+    // kernel's scheme, vtb_k7_lds.hip): lane b walks boundaries [b tbb, (b+1) tbb) back from
+    // a warm-up past its block's end, starting from state 0 there (exact when the walk starts
+    // at the last boundary).  A block is right if it entered on its successor's exit state and
+    // that successor is proven; failed blocks re-walk from a proven successor until all are
+    // proven.  Then every lane emits its block's windows (LDS atomic OR: windows share words).
+    if (!(a.dbg & 1)) {
+        const int nb = gen_boundaries(T, S), pstride = N < 4 ? 4 : N;
+        const int warm = (a.warm + S - 1) / S;
+        auto ptr = [&](int i, int s) -> int {  // state at boundary i-1 on the survivor of s at i
+            if (R == 4) return ptrs[size_t(i) * 256 + ((s & 63) << 2) + (s >> 6)];
+            return ptrs[size_t(i) * size_t(pstride) + s];
         };
-        const int tbb = (T + 63) / 64, lo = lane * tbb, top = min(lo + tbb, T);
-        const bool active = lo < T;
-        const int start = min(top + kGenWarm, T);
+        const int tbb = (nb + 63) / 64, lo = lane * tbb, top = min(lo + tbb, nb);
+        const bool active = lo < nb;
+        const int start = min(top + warm, nb);
         int s = 0;
-        for (int t = start - 1; active && t >= top; t--) s = pred(s, t);
+        for (int i = start - 1; active && i >= top; i--) s = ptr(i, s);
         int s_top = s;
-        for (int t = top - 1; active && t >= lo; t--) s = pred(s, t);
+        for (int i = top - 1; active && i >= lo; i--) s = ptr(i, s);
         int fin = s;
-        bool fixed = !active || start == T;
+        bool fixed = !active || start == nb;
         for (int round = 0; round < 65; round++) {
             const int sf = __shfl_down(fin, 1);
             const bool ok = fixed || s_top == sf;
@@ -267,35 +357,47 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
             if (bad == 0) break;
             if (!ok && (bad >> (lane + 1)) == 0) {
                 s_top = s = sf;
-                for (int t = top - 1; t >= lo; t--) s = pred(s, t);
+                for (int i = top - 1; i >= lo; i--) s = ptr(i, s);
                 fin = s;
                 fixed = true;
             }
         }
+        // window i holds the inputs of steps t_b + (i-1) S + 1 .. t_b + i S: the kS bits of the
+        // state at boundary i, oldest (its top bits) first, at stream bit p0 = (t_b + (i-1) S + 1) k
+        // (the first window's bits before step 0 are the start state's and dropped; the last
+        // window is the S flush steps and not emitted)
         uint32_t* ow = reinterpret_cast<uint32_t*>(outb);
+        const int tb0 = (T - 1) % S;
         uint32_t acc = 0;
         int wcur = -1;
-        s = s_top;
-        for (int t = top - 1; active && t >= lo; t--) {
-            if (t < T - a.S) {
-                const int seg = s & (E - 1);
-                for (int j = 0; j < k; j++) {
-                    if ((seg >> (k - 1 - j)) & 1) {
-                        const int pos = t * k + j;
-                        if ((pos >> 5) != wcur) {
-                            if (acc) atomicOr(ow + wcur, acc);
-                            wcur = pos >> 5, acc = 0;
-                        }
-                        acc |= 1u << (8 * ((pos >> 3) & 3) + 7 - (pos & 7));
-                    }
-                }
+        auto put = [&](int byte, uint32_t v) {
+            if ((byte >> 2) != wcur) {
+                if (acc) atomicOr(ow + wcur, acc);
+                wcur = byte >> 2, acc = 0;
             }
-            s = pred(s, t);
+            acc |= v << (8 * (byte & 3));
+        };
+        s = s_top;
+        for (int i = top - 1; active && i >= lo; i--) {
+            if (i < nb - 1) {
+                int p0 = (tb0 + (i - 1) * S + 1) * k, w = kS;
+                uint32_t fv = uint32_t(s);
+                if (p0 < 0) {
+                    w += p0;
+                    fv &= (1u << w) - 1u;
+                    p0 = 0;
+                }
+                const uint32_t v16 = fv << (16 - w - (p0 & 7));
+                const int byte = p0 >> 3;
+                if (v16 & 0xFFu) put(byte + 1, v16 & 0xFFu);
+                if (v16 >> 8) put(byte, v16 >> 8);
+            }
+            s = ptr(i, s);
         }
         if (acc) atomicOr(ow + wcur, acc);
     }
     __syncthreads();
-    uint8_t* orow = out + f * out_stride;  // (GDEC: each lane read the decision words its walks need)
+    uint8_t* orow = out + f * out_stride;  // (GDEC: each lane read the pointer bytes its walks need)
     for (int i = lane; i < (a.L + 7) / 8; i += 64) orow[i] = outb[i];
 }
 
@@ -322,11 +424,15 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     if (frames == 0) return VTB_OK;
     vtb::GenArgs a{};
     a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R, a.u8 = u8 ? 1 : 0;
+    a.dbg = vtb::debug_flags();
+    a.warm = 96;
+    if (const char* w = getenv("VTB_GENK_WARM")) a.warm = std::max(0, atoi(w));  // measurement only
     for (int i = 0; i < n; i++) a.rg[i] = vtb::gen_rev(code->generators[i], k * K);
-    // decision words in LDS while they leave room for 4 waves per CU, else in a workspace
-    const size_t dec_bytes = 8 * size_t(T) * R * k;
+    // survivor pointers in LDS while they leave room for 4 waves per CU, else in a workspace
+    const size_t dec_bytes = (vtb::gen_ptr_bytes(T, S, N) + 15) & ~size_t(15);
+    a.ptr_bytes = int(dec_bytes);
     const bool gdec = dec_bytes > 32 * 1024;
-    const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, R, k, gdec);
+    const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, S, gdec);
     if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
     vtb::note_kernel("genk");
@@ -349,7 +455,7 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     for (size_t f0 = 0; f0 < frames && rc == VTB_OK; f0 += chunk) {
         const size_t nf = std::min(chunk, frames - f0);
         hipLaunchKernelGGL(vtb::genk_kernel<true>, dim3(unsigned(nf)), dim3(64), ly.total, st, d_in + f0 * in_stride,
-                           in_stride, d_out + f0 * out_stride, out_stride, nf, a, ly, static_cast<uint64_t*>(ws));
+                           in_stride, d_out + f0 * out_stride, out_stride, nf, a, ly, static_cast<uint8_t*>(ws));
         rc = vtb::gen_status();
     }
     if (vtb::workspace_free(ws, st) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;

@@ -40,6 +40,30 @@ def test_genk_gpu_vs_oracle(orc, code, L, F, p):
         assert (got == unc).all()  # noise-free frames decode to their payload
 
 
+@pytest.mark.parametrize("code", GENK_CODES, ids=lambda c: f"k{c[0]}K{c[1]}n{len(c[2])}")
+def test_genk_gpu_window_phases(orc, code):
+    """Frame lengths of every residue T mod S (the first survivor-pointer window is partial,
+    or the boundaries fall on other steps) and of one and two segments."""
+    k, K, g = code
+    S = K - 1
+    for m in sorted({1, 2, 3, 5, 7, 11, 13, 2 * S + 1, 3 * S + 2, 64, 255}):
+        L = k * m
+        # received segments at random (any sequence is a valid decoder input; the encoder
+        # helpers work in whole payload bytes)
+        rng = np.random.default_rng(1000 + m)
+        coded = rng.integers(0, 1 << len(g), (9, m + S), dtype=np.uint8)
+        want = orc.genk_decode(k, K, g, coded, L)
+        xi = torch.from_numpy(coded).cuda()
+        out = torch.zeros((coded.shape[0], (L + 7) // 8), dtype=torch.uint8, device="cuda")
+        gk = native.VtbGenKCode.make(k, K, g)  # the C ABI: any multiple of k (GenKDecoder keeps 8 | L)
+        native.check(native.lib().vtb_genk_decode_device(ctypes.byref(gk), L, ctypes.c_void_p(xi.data_ptr()),
+                                                         xi.stride(0), ctypes.c_void_p(out.data_ptr()),
+                                                         out.stride(0), coded.shape[0], None), "vtb_genk_decode_device")
+        got = out.cpu().numpy()
+        bad = np.flatnonzero((got != want).any(axis=1))
+        assert bad.size == 0, (code, L, bad[:8])
+
+
 def test_genk_gpu_k1_golden_vectors():
     """k = 1, K = 7: the reference's own golden frames decode to the reference's output."""
     for key, L, unc, rx, dec in golden_sets(7):
