@@ -11,11 +11,11 @@
 // metrics and the reference's start metrics 0 / (uint8)(N+1) (:236-262); the checker is
 // oracle_genk_decode, and k = 1 reproduces the k=1 decoder bit for bit.
 //
-// One wave64 per frame.  The N = 2^(kS) <= 256 states spread over the lanes (state d in
-// lane d % 64, register d / 64); metrics double-buffered in LDS (each lane gathers its 2^k
-// predecessors with ds_read), decisions as k ballot words per register per step in LDS,
-// edge labels from an LDS table of the N * 2^k delays.  A completeness kernel: these codes
-// are not on the headline path, so it favours generality over the K=7 kernel's tricks.
+// One wave64 per frame.  The N = 2^(kS) <= 256 states spread over the lanes (N <= 64: state d
+// in lane d, predecessors by ds_bpermute; N = 256: states 4 lane .. 4 lane + 3, values
+// double-buffered in LDS), survivor pointers every S steps instead of per-step decisions
+// (below), a verified block-parallel traceback over them.  A completeness kernel: these codes
+// are not on the headline path.
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -127,13 +127,18 @@ __device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t
     const bool live = d < N;
     const uint32_t tag = live ? own_tag(d, kS, KB) : 0u;
     uint32_t v = live ? (uint32_t(met[d]) << kMetShift) | tag : 0u;
-    uint32_t lab[E];
+    constexpr bool LIN = !PK && !U8;  // as in acs_r4 below
+    uint32_t lab[E], be[E];
     int srcl[E];
+    const uint32_t labd = live ? uint32_t(tab[d]) : 0u;
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int src = live ? (d >> KB) | (e << (kS - KB)) : 0;
         srcl[e] = src << 2;
-        if (U8)  // butterfly j = d >> 1: symm[j] = label of delay (j << 1) | 0, complemented for ec
+        be[e] = LIN ? __builtin_amdgcn_readfirstlane(uint32_t(tab[e << kS])) : 0u;
+        if (LIN)
+            lab[e] = 0;
+        else if (U8)  // butterfly j = d >> 1: symm[j] = label of delay (j << 1) | 0, complemented for ec
             lab[e] = live ? uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u) : 0u;
         else
             lab[e] = live ? uint32_t(tab[(src << KB) | (d & (E - 1))]) : 0u;
@@ -148,7 +153,9 @@ __device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
         for (int e = 0; e < E; e++) {
-            uint32_t c = gen_cand<PK>(uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], int(v))), lab[e], rx, P);
+            const uint32_t pv = uint32_t(__builtin_amdgcn_ds_bpermute(srcl[e], int(v)));
+            uint32_t c = LIN ? gen_cand<false>(pv, labd, be[e] ^ __builtin_amdgcn_readfirstlane(rx), 0u)
+                             : gen_cand<PK>(pv, lab[e], rx, P);
             if (U8) c &= 0xFFFFFu;  // (pm + bm) mod 256
             best = min(best, c);
         }
@@ -170,29 +177,43 @@ __device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t
     }
 }
 
-// N = 256 states (k * S = 8: k = 1, 2 or 4), four states per lane: d = 64 r + lane.  The
-// 4 * 2^k edge labels of a lane's states are time-invariant and sit in registers (compile-time
-// indices: k is a template parameter), the previous values in LDS (double-buffered; the 2^k
-// predecessors of a lane's state r are one base address apart by compile-time offsets).
-// Pointers: a dword per lane and boundary, byte r = state 64 r + lane (gen_ptr below).
+// N = 256 states (k * S = 8: k = 1, 2 or 4), four consecutive states per lane: d = 4 lane + r.
+// Their predecessors src = d / 2^k + e 2^(8-k) then coincide: at k = 2 and 4 all four states
+// of a lane share the same 2^k predecessors (lane + 64 e; lane / 4 + 16 e), at k = 1 pairs do
+// (2 lane + r / 2 + 128 e), so a lane reads 4, 4 or 16 values per step instead of 4 * 2^k,
+// and writes its four new values as one 16-byte store.  The values live in LDS (double-
+// buffered, state s at s); the 4 * 2^k edge labels of a lane's states are time-invariant and
+// sit in registers (k is a template parameter: every per-edge loop unrolls).  Pointers: the
+// lane's four bytes form one dword, so boundary i's 256 bytes are in state order.
 template <int KB, bool U8 = false, bool PK = false>
 __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
                                        uint32_t* met, uint32_t* ptr32, int lane) {
     constexpr int E = 1 << KB, kS = 8, N = 256, S = 8 / KB;
-    uint32_t lab[4][E], tag[4];
-    int sbase[4];
+    constexpr int G = KB == 1 ? 2 : 1;  // distinct predecessor sets per lane
+    // LIN (neither packed nor U8): the label of edge (e -> d) is tab[d | e << kS] = tab[d] ^
+    // tab[e << kS] (the encoder is linear over GF(2)), so a lane keeps its states' tab[d] (4
+    // registers) and the step's uniform y_e = tab[e << kS] ^ rx sits in scalar registers,
+    // instead of 4 * 2^k label registers (64 at k = 4: the wave count per SIMD)
+    constexpr bool LIN = !PK && !U8;
+    uint32_t lab[4][LIN ? 1 : E], tag[4], be[E];
+    const int base = KB == 4 ? lane >> 2 : lane << (2 - KB);  // + g: the lane's predecessor sets
+#pragma unroll
+    for (int e = 0; e < E; e++) be[e] = LIN ? __builtin_amdgcn_readfirstlane(uint32_t(tab[e << kS])) : 0u;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        const int d = r * 64 + lane;
-        sbase[r] = d >> KB;
+        const int d = 4 * lane + r;
         tag[r] = own_tag(d, kS, KB);
-        met[r * 64 + lane] = (met[r * 64 + lane] << kMetShift) | tag[r];
+        met[d] = (met[d] << kMetShift) | tag[r];
+        if (LIN) {
+            lab[r][0] = tab[d];
+            continue;
+        }
 #pragma unroll
-        for (int e = 0; e < E; e++) {
+        for (int e = 0; e < (LIN ? 1 : E); e++) {
             if (U8)  // the butterfly identity of acs_r1 U8
                 lab[r][e] = uint32_t(tab[(d >> 1) << 1]) ^ ((((d & 1) ^ e) & 1) ? nmask : 0u);
             else
-                lab[r][e] = uint32_t(tab[(((d >> KB) | (e << (kS - KB))) << KB) | (d & (E - 1))]);
+                lab[r][e] = uint32_t(tab[d | (e << kS)]);
             if (PK) lab[r][e] *= 4;
         }
     }
@@ -211,14 +232,21 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
         uint32_t* mn = met + (cur ^ 1) * N;
         const bool bnd = cnt == S - 1;
         cnt = bnd ? 0 : cnt + 1;
-        uint32_t nm[4];
+        uint32_t pv[G][E], y[E], nm[4];
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+            for (int e = 0; e < E; e++) pv[g][e] = mc[base + g + (e << (kS - KB))];
+#pragma unroll
+        for (int e = 0; e < E; e++) y[e] = LIN ? be[e] ^ __builtin_amdgcn_readfirstlane(rx) : 0u;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const uint32_t* ps = mc + sbase[r];  // predecessor e at ps[e << (kS - KB)]
+            const int g = KB == 1 ? r >> 1 : 0;
             uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
             for (int e = 0; e < E; e++) {
-                uint32_t c = gen_cand<PK>(ps[e << (kS - KB)], lab[r][e], rx, P);
+                uint32_t c = LIN ? gen_cand<false>(pv[g][e], lab[r][0], y[e], 0u)
+                                 : gen_cand<PK>(pv[g][e], lab[r][e], rx, P);
                 if (U8) c &= 0xFFFFFu;
                 best = min(best, c);
             }
@@ -241,8 +269,7 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
                 renorm++;
             }
         }
-#pragma unroll
-        for (int r = 0; r < 4; r++) mn[r * 64 + lane] = nm[r];
+        reinterpret_cast<uint4*>(mn)[lane] = make_uint4(nm[0], nm[1], nm[2], nm[3]);
         cur ^= 1;
         // one wave per workgroup: its LDS accesses complete in issue order, so the next step's
         // reads see these writes without a workgroup barrier (a compiler fence keeps the order)
@@ -253,7 +280,7 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
 
 // GDEC: pointer bytes in a global workspace (one slot per frame of the launch) instead of
 // LDS, for trellises whose pointers would hold the CU to few waves.
-template <bool GDEC>
+template <bool GDEC, int KB>
 __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                   uint8_t* __restrict__ out, size_t out_stride, size_t frames,
                                                   GenArgs a, GenLayout ly, uint8_t* __restrict__ ws) {
@@ -267,7 +294,8 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     const int lane = threadIdx.x;
     const size_t f = blockIdx.x;
     if (f >= frames) return;
-    const int k = a.k, N = a.N, E = 1 << k, S = a.S, kS = k * S, T = a.T, R = a.R, n = a.n;
+    constexpr int k = KB, E = 1 << KB;  // one instance per k: each gets its own register budget
+    const int N = a.N, S = a.S, kS = k * S, T = a.T, R = a.R, n = a.n;
     const uint32_t nmask = (1u << n) - 1u;
 
     for (int i = lane; i < N * E; i += 64) {  // edge labels, index = delay (src << k) | bits
@@ -276,7 +304,9 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         tab[i] = uint8_t(o);
     }
     const uint8_t* row = in + f * in_stride;
+#pragma unroll 1
     for (int i = lane; i <= T; i += 64) inb[i] = i < T ? row[i] : 0;
+#pragma unroll 1
     for (int i = lane; i < (a.L + 7) / 8; i += 64) outb[i] = 0;
     const uint32_t init = uint8_t(N + 1);
     for (int d = lane; d < N; d += 64) met[d] = d == 0 ? 0 : init;
@@ -286,44 +316,21 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     if (a.dbg & 2) {
     } else if (R == 1) {
         const int32_t* m0 = reinterpret_cast<const int32_t*>(met);
-        switch (k) {
-            case 1:
-                if (a.u8)
-                    pk ? acs_r1<1, true, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
-                       : acs_r1<1, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
-                else
-                    pk ? acs_r1<1, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
-                       : acs_r1<1>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
-                break;
-            case 2:
-                pk ? acs_r1<2, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
-                   : acs_r1<2>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
-                break;
-            case 3:
-                pk ? acs_r1<3, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
-                   : acs_r1<3>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
-                break;
-            default:
-                pk ? acs_r1<4, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
-                   : acs_r1<4>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
-                break;
-        }
-    } else {
+        if (KB == 1 && a.u8)
+            pk ? acs_r1<KB, true, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+               : acs_r1<KB, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+        else
+            pk ? acs_r1<KB, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
+               : acs_r1<KB, false>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+    } else if constexpr (KB == 1 || KB == 2 || KB == 4) {
         uint32_t* p32 = reinterpret_cast<uint32_t*>(ptrs);
-        if (k == 1) {
-            if (a.u8)
-                pk ? acs_r4<1, true, true>(T, n, inb, nmask, tab, met, p32, lane)
-                   : acs_r4<1, true>(T, n, inb, nmask, tab, met, p32, lane);
-            else
-                pk ? acs_r4<1, false, true>(T, n, inb, nmask, tab, met, p32, lane)
-                   : acs_r4<1>(T, n, inb, nmask, tab, met, p32, lane);
-        } else if (k == 2) {
-            pk ? acs_r4<2, false, true>(T, n, inb, nmask, tab, met, p32, lane)
-               : acs_r4<2>(T, n, inb, nmask, tab, met, p32, lane);
-        } else {
-            pk ? acs_r4<4, false, true>(T, n, inb, nmask, tab, met, p32, lane)
-               : acs_r4<4>(T, n, inb, nmask, tab, met, p32, lane);
-        }
+        // (k = 4: 64 packed-label registers would cost waves; the linear labels need 4)
+        if (KB == 1 && a.u8)
+            pk ? acs_r4<KB, true, true>(T, n, inb, nmask, tab, met, p32, lane)
+               : acs_r4<KB, true>(T, n, inb, nmask, tab, met, p32, lane);
+        else
+            pk && KB != 4 ? acs_r4<KB, false, KB != 4>(T, n, inb, nmask, tab, met, p32, lane)
+                          : acs_r4<KB, false>(T, n, inb, nmask, tab, met, p32, lane);
     }
     __syncthreads();
 
@@ -338,8 +345,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         const int nb = gen_boundaries(T, S), pstride = N < 4 ? 4 : N;
         const int warm = (a.warm + S - 1) / S;
         auto ptr = [&](int i, int s) -> int {  // state at boundary i-1 on the survivor of s at i
-            if (R == 4) return ptrs[size_t(i) * 256 + ((s & 63) << 2) + (s >> 6)];
-            return ptrs[size_t(i) * size_t(pstride) + s];
+            return ptrs[size_t(i) * size_t(pstride) + s];  // (R = 4: the lanes' dwords are in state order)
         };
         const int tbb = (nb + 63) / 64, lo = lane * tbb, top = min(lo + tbb, nb);
         const bool active = lo < nb;
@@ -398,6 +404,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
     }
     __syncthreads();
     uint8_t* orow = out + f * out_stride;  // (GDEC: each lane read the pointer bytes its walks need)
+#pragma unroll 1  // (unrolled, the byte copy would set the kernel's register count)
     for (int i = lane; i < (a.L + 7) / 8; i += 64) orow[i] = outb[i];
 }
 
@@ -436,14 +443,32 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
     vtb::note_kernel("genk");
+    const auto kern = [&](bool g) -> const void* {
+        switch (k) {
+            case 1: return g ? reinterpret_cast<const void*>(vtb::genk_kernel<true, 1>)
+                             : reinterpret_cast<const void*>(vtb::genk_kernel<false, 1>);
+            case 2: return g ? reinterpret_cast<const void*>(vtb::genk_kernel<true, 2>)
+                             : reinterpret_cast<const void*>(vtb::genk_kernel<false, 2>);
+            case 3: return g ? reinterpret_cast<const void*>(vtb::genk_kernel<true, 3>)
+                             : reinterpret_cast<const void*>(vtb::genk_kernel<false, 3>);
+            default: return g ? reinterpret_cast<const void*>(vtb::genk_kernel<true, 4>)
+                              : reinterpret_cast<const void*>(vtb::genk_kernel<false, 4>);
+        }
+    };
+    const auto launch = [&](bool g, size_t f0, size_t nf, uint8_t* ws) {
+        const uint8_t* pin = d_in + f0 * in_stride;
+        uint8_t* pout = d_out + f0 * out_stride;
+        void* args[] = {&pin, const_cast<size_t*>(&in_stride), &pout, const_cast<size_t*>(&out_stride), &nf,
+                        &a, const_cast<vtb::GenLayout*>(&ly), &ws};
+        if (hipLaunchKernel(kern(g), dim3(unsigned(nf)), dim3(64), args, ly.total, st) != hipSuccess)
+            return VTB_ERR_DEVICE;
+        return vtb::gen_status();
+    };
     if (!gdec) {
         if (ly.total > 64 * 1024 &&
-            hipFuncSetAttribute(reinterpret_cast<const void*>(vtb::genk_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, int(ly.total)) != hipSuccess)
+            hipFuncSetAttribute(kern(false), hipFuncAttributeMaxDynamicSharedMemorySize, int(ly.total)) != hipSuccess)
             return VTB_ERR_DEVICE;
-        hipLaunchKernelGGL(vtb::genk_kernel<false>, dim3(unsigned(frames)), dim3(64), ly.total, st, d_in, in_stride,
-                           d_out, out_stride, frames, a, ly, nullptr);
-        return vtb::gen_status();
+        return launch(false, 0, frames, nullptr);
     }
     // workspace from the stream's pool, up to 1 GiB per launch (frames in launches of that)
     const size_t per = std::max<size_t>(1, (size_t(1) << 30) / dec_bytes);
@@ -452,12 +477,8 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     void* ws = nullptr;
     if (vtb::workspace_alloc(&ws, chunk * dec_bytes, st) != hipSuccess) return VTB_ERR_NOMEM;
     int rc = VTB_OK;
-    for (size_t f0 = 0; f0 < frames && rc == VTB_OK; f0 += chunk) {
-        const size_t nf = std::min(chunk, frames - f0);
-        hipLaunchKernelGGL(vtb::genk_kernel<true>, dim3(unsigned(nf)), dim3(64), ly.total, st, d_in + f0 * in_stride,
-                           in_stride, d_out + f0 * out_stride, out_stride, nf, a, ly, static_cast<uint8_t*>(ws));
-        rc = vtb::gen_status();
-    }
+    for (size_t f0 = 0; f0 < frames && rc == VTB_OK; f0 += chunk)
+        rc = launch(true, f0, std::min(chunk, frames - f0), static_cast<uint8_t*>(ws));
     if (vtb::workspace_free(ws, st) != hipSuccess && rc == VTB_OK) rc = VTB_ERR_DEVICE;
     return rc;
 }

@@ -101,7 +101,8 @@ def test_plan_without_gpu_fails_loudly():
     k9 = native.VtbCode.make(9, CODES[9])
     assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k9), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
     k5 = native.VtbCode.make(5, CODES[5])
-    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k5), 0, 8, 0, 0) == native.VTB_ERR_UNSUPPORTED
+    # every K streams since round 3 (the generic stream kernel): no GPU -> device error, loudly
+    assert lib.vtb_stream_create(ctypes.byref(stream), ctypes.byref(k5), 0, 8, 0, 0) == native.VTB_ERR_DEVICE
 
 
 @pytest.mark.parametrize("F", [0, 1, 2, 3, 7, 100, 1001, 4096, 131072, 2**20, 2**20 + 5, 2**40 + 3])
