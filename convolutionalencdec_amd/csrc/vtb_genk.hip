@@ -127,7 +127,7 @@ __device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t
     const bool live = d < N;
     const uint32_t tag = live ? own_tag(d, kS, KB) : 0u;
     uint32_t v = live ? (uint32_t(met[d]) << kMetShift) | tag : 0u;
-    constexpr bool LIN = !PK && !U8;  // as in acs_r4 below
+    constexpr bool LIN = !PK && !U8;  // as in acs_rn below
     uint32_t lab[E], be[E];
     int srcl[E];
     const uint32_t labd = live ? uint32_t(tab[d]) : 0u;
@@ -177,31 +177,33 @@ __device__ __forceinline__ void acs_r1(int N, int S, int T, int n, const uint8_t
     }
 }
 
-// N = 256 states (k * S = 8: k = 1, 2 or 4), four consecutive states per lane: d = 4 lane + r.
-// Their predecessors src = d / 2^k + e 2^(8-k) then coincide: at k = 2 and 4 all four states
-// of a lane share the same 2^k predecessors (lane + 64 e; lane / 4 + 16 e), at k = 1 pairs do
-// (2 lane + r / 2 + 128 e), so a lane reads 4, 4 or 16 values per step instead of 4 * 2^k,
-// and writes its four new values as one 16-byte store.  The values live in LDS (double-
-// buffered, state s at s); the 4 * 2^k edge labels of a lane's states are time-invariant and
-// sit in registers (k is a template parameter: every per-edge loop unrolls).  Pointers: the
-// lane's four bytes form one dword, so boundary i's 256 bytes are in state order.
-template <int KB, bool U8 = false, bool PK = false>
-__device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
-                                       uint32_t* met, uint32_t* ptr32, int lane) {
-    constexpr int E = 1 << KB, kS = 8, N = 256, S = 8 / KB;
-    constexpr int G = KB == 1 ? 2 : 1;  // distinct predecessor sets per lane
+// N = 64 R states, R = 2 (k = 1, K = 8) or 4 (k S = 8: k = 1, 2 or 4), R consecutive states per
+// lane: d = R lane + r.  Their predecessors src = d / 2^k + e 2^(kS-k) then coincide: at
+// R = 4 and k = 2, 4 all four states of a lane share the same 2^k predecessors (lane + 64 e;
+// lane / 4 + 16 e), at k = 1 pairs do (2 lane + r / 2 + 128 e; R = 2: lane + 64 e), so a lane
+// reads 4, 4, 16 or 2 values per step instead of R 2^k, and writes its R new values as one
+// 16- or 8-byte store.  The values live in LDS (double-buffered, state s at s); the R 2^k
+// edge labels of a lane's states are time-invariant and sit in registers (k is a template
+// parameter: every per-edge loop unrolls).  Pointers: the lane's R bytes form one dword or
+// halfword, so boundary i's N bytes are in state order.
+template <int KB, int R, bool U8 = false, bool PK = false>
+__device__ __forceinline__ void acs_rn(int T, int n, const uint8_t* inb, uint32_t nmask, const uint8_t* tab,
+                                       uint32_t* met, uint8_t* ptrs, int lane) {
+    static_assert(R == 4 || (R == 2 && KB == 1), "N = 128 only at k = 1");
+    constexpr int E = 1 << KB, kS = R == 4 ? 8 : 7, N = 64 * R, S = kS / KB;
+    constexpr int G = (R >> KB) > 1 ? (R >> KB) : 1;  // distinct predecessor sets per lane
     // LIN (neither packed nor U8): the label of edge (e -> d) is tab[d | e << kS] = tab[d] ^
     // tab[e << kS] (the encoder is linear over GF(2)), so a lane keeps its states' tab[d] (4
     // registers) and the step's uniform y_e = tab[e << kS] ^ rx sits in scalar registers,
     // instead of 4 * 2^k label registers (64 at k = 4: the wave count per SIMD)
     constexpr bool LIN = !PK && !U8;
-    uint32_t lab[4][LIN ? 1 : E], tag[4], be[E];
-    const int base = KB == 4 ? lane >> 2 : lane << (2 - KB);  // + g: the lane's predecessor sets
+    uint32_t lab[R][LIN ? 1 : E], tag[R], be[E];
+    const int base = (R * lane) >> KB;  // + g: the lane's predecessor sets
 #pragma unroll
     for (int e = 0; e < E; e++) be[e] = LIN ? __builtin_amdgcn_readfirstlane(uint32_t(tab[e << kS])) : 0u;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int d = 4 * lane + r;
+    for (int r = 0; r < R; r++) {
+        const int d = R * lane + r;
         tag[r] = own_tag(d, kS, KB);
         met[d] = (met[d] << kMetShift) | tag[r];
         if (LIN) {
@@ -232,7 +234,7 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
         uint32_t* mn = met + (cur ^ 1) * N;
         const bool bnd = cnt == S - 1;
         cnt = bnd ? 0 : cnt + 1;
-        uint32_t pv[G][E], y[E], nm[4];
+        uint32_t pv[G][E], y[E], nm[R];
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
@@ -240,8 +242,8 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
 #pragma unroll
         for (int e = 0; e < E; e++) y[e] = LIN ? be[e] ^ __builtin_amdgcn_readfirstlane(rx) : 0u;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int g = KB == 1 ? r >> 1 : 0;
+        for (int r = 0; r < R; r++) {
+            const int g = G > 1 ? r >> KB : 0;
             uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
             for (int e = 0; e < E; e++) {
@@ -253,23 +255,33 @@ __device__ __forceinline__ void acs_r4(int T, int n, const uint8_t* inb, uint32_
             nm[r] = best;
         }
         if (bnd) {
-            ptr32[size_t(bi) * 64 + lane] = __builtin_amdgcn_perm(nm[1], nm[0], 0x0c0c0400u) |
-                                            __builtin_amdgcn_perm(nm[3], nm[2], 0x04000c0cu);
+            const uint32_t lo = __builtin_amdgcn_perm(nm[1], nm[0], 0x0c0c0400u);
+            if constexpr (R == 4)
+                reinterpret_cast<uint32_t*>(ptrs)[size_t(bi) * 64 + lane] =
+                    lo | __builtin_amdgcn_perm(nm[R - 1], nm[R - 2], 0x04000c0cu);
+            else
+                reinterpret_cast<uint16_t*>(ptrs)[size_t(bi) * 64 + lane] = uint16_t(lo);
             bi++;
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++) nm[r] = gen_next(nm[r], tag[r], bnd);
+        for (int r = 0; r < R; r++) nm[r] = gen_next(nm[r], tag[r], bnd);
         if (U8) {
             if (renorm >= 120) {
-                const uint32_t mn4 = wave_min(min(min(nm[0], nm[1]), min(nm[2], nm[3]))) & ~0xFFFu;
+                uint32_t mr = nm[0];
 #pragma unroll
-                for (int r = 0; r < 4; r++) nm[r] -= mn4;
+                for (int r = 1; r < R; r++) mr = min(mr, nm[r]);
+                mr = wave_min(mr) & ~0xFFFu;
+#pragma unroll
+                for (int r = 0; r < R; r++) nm[r] -= mr;
                 renorm = 0;
             } else {
                 renorm++;
             }
         }
-        reinterpret_cast<uint4*>(mn)[lane] = make_uint4(nm[0], nm[1], nm[2], nm[3]);
+        if constexpr (R == 4)
+            reinterpret_cast<uint4*>(mn)[lane] = make_uint4(nm[0], nm[1], nm[R - 2], nm[R - 1]);
+        else
+            reinterpret_cast<uint2*>(mn)[lane] = make_uint2(nm[0], nm[1]);
         cur ^= 1;
         // one wave per workgroup: its LDS accesses complete in issue order, so the next step's
         // reads see these writes without a workgroup barrier (a compiler fence keeps the order)
@@ -322,15 +334,23 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         else
             pk ? acs_r1<KB, false, true>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane)
                : acs_r1<KB, false>(N, S, T, n, inb, nmask, tab, m0, ptrs, lane);
+    } else if (R == 2) {  // k = 1, K = 8
+        if constexpr (KB == 1) {
+            if (a.u8)
+                pk ? acs_rn<1, 2, true, true>(T, n, inb, nmask, tab, met, ptrs, lane)
+                   : acs_rn<1, 2, true>(T, n, inb, nmask, tab, met, ptrs, lane);
+            else
+                pk ? acs_rn<1, 2, false, true>(T, n, inb, nmask, tab, met, ptrs, lane)
+                   : acs_rn<1, 2, false>(T, n, inb, nmask, tab, met, ptrs, lane);
+        }
     } else if constexpr (KB == 1 || KB == 2 || KB == 4) {
-        uint32_t* p32 = reinterpret_cast<uint32_t*>(ptrs);
         // (k = 4: 64 packed-label registers would cost waves; the linear labels need 4)
         if (KB == 1 && a.u8)
-            pk ? acs_r4<KB, true, true>(T, n, inb, nmask, tab, met, p32, lane)
-               : acs_r4<KB, true>(T, n, inb, nmask, tab, met, p32, lane);
+            pk ? acs_rn<KB, 4, true, true>(T, n, inb, nmask, tab, met, ptrs, lane)
+               : acs_rn<KB, 4, true>(T, n, inb, nmask, tab, met, ptrs, lane);
         else
-            pk && KB != 4 ? acs_r4<KB, false, KB != 4>(T, n, inb, nmask, tab, met, p32, lane)
-                          : acs_r4<KB, false>(T, n, inb, nmask, tab, met, p32, lane);
+            pk && KB != 4 ? acs_rn<KB, 4, false, KB != 4>(T, n, inb, nmask, tab, met, ptrs, lane)
+                          : acs_rn<KB, 4, false>(T, n, inb, nmask, tab, met, ptrs, lane);
     }
     __syncthreads();
 
@@ -345,7 +365,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         const int nb = gen_boundaries(T, S), pstride = N < 4 ? 4 : N;
         const int warm = (a.warm + S - 1) / S;
         auto ptr = [&](int i, int s) -> int {  // state at boundary i-1 on the survivor of s at i
-            return ptrs[size_t(i) * size_t(pstride) + s];  // (R = 4: the lanes' dwords are in state order)
+            return ptrs[size_t(i) * size_t(pstride) + s];  // (R > 1: the lanes' words are in state order)
         };
         const int tbb = (nb + 63) / 64, lo = lane * tbb, top = min(lo + tbb, nb);
         const bool active = lo < nb;

@@ -1,5 +1,5 @@
 """Golden vectors for k = 1 codes with n != 2 (tests/golden/k1n.npz), produced by the
-reference itself: oracle/_ref/libref_{k7n3,k9n3,k5n4}.so are the reference's own
+reference itself: oracle/_ref/libref_{k7n3,k9n3,k5n4,k8n3}.so are the reference's own
 src/*.c compiled by oracle/Makefile with params/<name> (K and n compile-time, as the
 reference's per-harness config directories).  Run in the build container only:
 
@@ -21,7 +21,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF_DIR = os.path.join(REPO, "oracle", "_ref")
 
 K1N = {"k7n3": (7, (0o133, 0o171, 0o165)), "k9n3": (9, (0o557, 0o663, 0o711)),
-       "k5n4": (5, (0o23, 0o35, 0o27, 0o33))}
+       "k5n4": (5, (0o23, 0o35, 0o27, 0o33)), "k8n3": (8, (0o225, 0o331, 0o367))}
 
 
 def ptr(a):

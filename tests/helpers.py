@@ -288,11 +288,11 @@ GENK_CODES = (
 )
 GENK_REF_PARAMS = {"k4_k2n3": GENK_CODES[0], "k3_k3n4": GENK_CODES[1]}
 
-# k = 1 codes with n != 2 (params/k7n3, k9n3, k5n4): the reference decoder is generic in n
+# k = 1 codes with n != 2 (params/k7n3, k9n3, k5n4, k8n3): the reference decoder is generic in n
 # (viterbiDecoderButterflyk1.c:104-107); oracle/_ref/libref_<name>.so is the reference built
 # with each, tests/golden/k1n.npz its outputs.
 K1N_PARAMS = {"k7n3": (7, (0o133, 0o171, 0o165)), "k9n3": (9, (0o557, 0o663, 0o711)),
-              "k5n4": (5, (0o23, 0o35, 0o27, 0o33))}
+              "k5n4": (5, (0o23, 0o35, 0o27, 0o33)), "k8n3": (8, (0o225, 0o331, 0o367))}
 
 
 def k1n_frames(orc, K, g, L, F, p, seed, garbage=False):

@@ -101,3 +101,68 @@ def test_genk_gpu_strided_rows(orc):
     got = out.cpu().numpy()
     assert (got[:, L // 8:] == 0xA5).all()
     assert (got[:, :L // 8] == orc.genk_decode(k, K, g, coded, L)).all()
+
+
+def _random_codes(seed, count):
+    """Random (k, K, generators) inside the C ABI's limits (k (K-1) <= 8, k K <= 12, n <= 8):
+    every ACS path of the kernel -- N <= 64 and N = 256, packed (n <= 3) and linear labels."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < count:
+        k = int(rng.integers(1, 5))
+        K = int(rng.integers(2, 8 // k + 2))
+        if k * (K - 1) > 8 or k * K > 12:
+            continue
+        n = int(rng.integers(1, 9))
+        g = tuple(int(v) for v in rng.integers(1, 1 << (k * K), n))
+        out.append((k, K, g))
+    return out
+
+
+@pytest.mark.parametrize("code", _random_codes(20261017, 40), ids=lambda c: f"k{c[0]}K{c[1]}n{len(c[2])}")
+def test_genk_gpu_random_codes(orc, code):
+    """Random codes (any generator set, n = 1..8, incl. catastrophic and repeated generators),
+    random received segments and encoded noisy frames, several lengths: bit for bit against
+    oracle_genk_decode."""
+    k, K, g = code
+    S, n = K - 1, len(g)
+    rng = np.random.default_rng(sum(g) + 31 * k + K)
+    for m in (1, 7, 64, 517):
+        L = k * m
+        coded = rng.integers(0, 1 << n, (6, m + S), dtype=np.uint8)
+        if L % 8 == 0:  # encoded frames with light noise (decisions not all ties)
+            _, enc = genk_frames(orc, k, K, g, L, 3, 0.03, m)
+            coded = np.concatenate([coded, enc])
+        want = orc.genk_decode(k, K, g, coded, L)
+        xi = torch.from_numpy(coded).cuda()
+        out = torch.zeros((coded.shape[0], (L + 7) // 8), dtype=torch.uint8, device="cuda")
+        gk = native.VtbGenKCode.make(k, K, g)
+        native.check(native.lib().vtb_genk_decode_device(ctypes.byref(gk), L, ctypes.c_void_p(xi.data_ptr()),
+                                                         xi.stride(0), ctypes.c_void_p(out.data_ptr()),
+                                                         out.stride(0), coded.shape[0], None), "vtb_genk_decode_device")
+        got = out.cpu().numpy()
+        bad = np.flatnonzero((got != want).any(axis=1))
+        assert bad.size == 0, (code, L, bad[:8])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_genk_gpu_random_k1_reference_u8(orc, seed):
+    """k = 1 in the reference's uint8 butterfly arithmetic (VTB_GENK_K1_REFERENCE_U8) for
+    random codes of K = 3..9, n = 1..8 (sums that wrap mod 256 for n >= 4), against
+    oracle_k1n_decode."""
+    rng = np.random.default_rng(700 + seed)
+    for _ in range(4):
+        K = int(rng.integers(3, 10))
+        n = int(rng.integers(1, 9))
+        g = tuple(int(v) for v in rng.integers(1, 1 << K, n))
+        L = int(rng.integers(1, 700))
+        coded = rng.integers(0, 256, (5, L + K - 1), dtype=np.uint8)  # garbage high bits too
+        want = orc.k1n_decode(K, g, coded, L)
+        code = native.VtbGenKCode.make(1, K, g, native.VTB_GENK_K1_REFERENCE_U8)
+        xi = torch.from_numpy(coded).cuda()
+        out = torch.zeros((coded.shape[0], (L + 7) // 8), dtype=torch.uint8, device="cuda")
+        native.check(native.lib().vtb_genk_decode_device(ctypes.byref(code), L, ctypes.c_void_p(xi.data_ptr()),
+                                                         xi.stride(0), ctypes.c_void_p(out.data_ptr()),
+                                                         out.stride(0), coded.shape[0], None), "vtb_genk_decode_device")
+        got = out.cpu().numpy()
+        assert (got == want).all(), (K, g, L)

@@ -1,6 +1,6 @@
 """k = 1 codes with n != 2 on the GPU.
 
-* The legacy drop-in built for params/k7n3, k9n3 and k5n4 (libviterbi_legacy_<name>.so)
+* The legacy drop-in built for params/k7n3, k9n3, k5n4 and k8n3 (libviterbi_legacy_<name>.so)
   decodes the reference's golden frames (tests/golden/k1n.npz, produced by the reference
   compiled with the same params) through VITERBI_DECODER_HARD exactly, with the reference's
   byte count, and nodeMetricsCur after every 7-segment last=false chunk equals the

@@ -21,7 +21,7 @@ from helpers import CODES, GENK_REF_PARAMS, Oracle, genk_frames, legacy_layout, 
 pytestmark = pytest.mark.gpu
 
 CONFIGS = {"k7": (1, 7, 2), "k9": (1, 9, 2), "k4_k2n3": (2, 4, 3), "k3_k3n4": (3, 3, 4),
-           "k7n3": (1, 7, 3), "k9n3": (1, 9, 3), "k5n4": (1, 5, 4)}
+           "k7n3": (1, 7, 3), "k9n3": (1, 9, 3), "k5n4": (1, 5, 4), "k8n3": (1, 8, 3)}
 
 
 @pytest.fixture(scope="module")
