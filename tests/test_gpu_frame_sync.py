@@ -96,15 +96,25 @@ def test_pure_noise_falls_back(orc, monkeypatch):
     assert s1[1] > s0[1]
 
 
-@pytest.mark.parametrize("K", [5])
-def test_other_k_frame_kernel(orc, K, monkeypatch):
+@pytest.mark.parametrize("K", [3, 4, 5, 6, 8])
+@pytest.mark.parametrize("soft", [False, True])
+def test_other_k_frame_kernel(orc, K, soft, monkeypatch):
+    """K without a single-frame kernel of its own (the generic path, one frame per call), with
+    a generator pair of both end taps drawn at random per K."""
     monkeypatch.delenv("VTB_KERNEL", raising=False)
-    L = 1000
-    unc, rx = random_frames(orc, K, L, 3, 0.03, seed=K)
-    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
-    s0 = seg_stats()
-    assert (run(d, rx) == orc.decode(K, CODES[K], rx, L)).all()
-    assert seg_stats()[2] - s0[2] == 3
+    rng = np.random.default_rng(40 + K)
+    g = CODES[K] if K == 5 else tuple(int(1 | (1 << (K - 1)) | (int(rng.integers(0, 1 << K)) & ((1 << (K - 1)) - 2)))
+                                      for _ in range(2))
+    for L in (1, 77, 1000):
+        if soft:
+            unc, rx = random_frames(orc, K, L, 3, 0.0, seed=K + L, soft=True, sigma=0.6, g=g)
+            rx = rx.reshape(3, -1)
+        else:
+            unc, rx = random_frames(orc, K, L, 3, 0.03, seed=K + L, g=g)
+        d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
+        s0 = seg_stats()
+        assert (run(d, rx) == orc.decode(K, g, rx, L, soft=soft)).all(), (K, g, L)
+        assert seg_stats()[2] - s0[2] == 3
 
 
 def test_k9_golden_vectors(monkeypatch):

@@ -225,3 +225,38 @@ def test_genk_random_vs_oracle(orc, case):
     got = GenKDecoder(k, K, g, L).decode_device(torch.from_numpy(coded).cuda()).cpu().numpy()
     bad = np.flatnonzero((got != want).any(axis=1))
     assert bad.size == 0, (case, bad.size, bad[:8])
+
+
+def _generator_cases(n=40, seed=20261017):
+    """Every constraint length of the batch decoder (K = 3..9: the generic LDS path at K = 3-6
+    and 8, the K=7 and K=9 kernels) with random generator pairs that have both end taps (the
+    reference's symmetric-butterfly requirement, viterbiDecoder.c:17-25)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        K = int(rng.integers(3, 10))
+        g = tuple(int(1 | (1 << (K - 1)) | (int(rng.integers(0, 1 << K)) & ((1 << (K - 1)) - 2))) for _ in range(2))
+        L = int(rng.integers(1, 2100))
+        F = int(rng.choice([1, 3, 64, 255, 700]))
+        soft = bool(rng.integers(0, 2))
+        noise = float(rng.choice([0.0, 0.05, 0.5]))
+        out.append((i, K, g, L, F, soft, noise))
+    return out
+
+
+@pytest.mark.parametrize("case", _generator_cases(),
+                         ids=lambda c: f"{c[0]}-K{c[1]}-g{c[2][0]:o}_{c[2][1]:o}-L{c[3]}-F{c[4]}-{'soft' if c[5] else 'hard'}")
+def test_random_generators_vs_oracle(orc, case):
+    i, K, g, L, F, soft, noise = case
+    if soft:
+        sigma = {0.0: 0.3, 0.05: 0.6, 0.5: 4.0}[noise]
+        unc, x = random_frames(orc, K, L, F, 0.0, 5000 + i, soft=True, sigma=sigma, g=g)
+    else:
+        unc, x = random_frames(orc, K, L, F, noise, 5000 + i, g=g)
+    x = np.ascontiguousarray(x).reshape(F, -1)
+    want = orc.decode(K, g, x, L, soft=soft, threads=THREADS)
+    got = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft).decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, (case, bad.size, bad[:8])
+    if noise == 0.0:
+        assert (got == unc).all()
