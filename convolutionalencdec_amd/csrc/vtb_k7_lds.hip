@@ -146,6 +146,19 @@ __device__ __forceinline__ void tstamp(const Launch& table, int k) {
     if (table.tstamp && threadIdx.x == 0) table.tstamp[8 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
 }
 
+// LDS byte address of a pointer into the shared-memory aperture
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return uint32_t(size_t((const __attribute__((address_space(3))) uint8_t*)p));
+}
+// a table column by its LDS byte address: col[i] is the i-th 8-byte (V, W) slot
+struct LdsCol {
+    uint32_t a;
+    __device__ __forceinline__ uint2 operator[](int i) const {
+        const unsigned long long v = *(const __attribute__((address_space(3))) unsigned long long*)size_t(a + 8u * uint32_t(i));
+        return make_uint2(uint32_t(v), uint32_t(v >> 32));
+    }
+};
+
 // lane <-> location map (an involution)
 __host__ __device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ (((l >> 2) & 1u) * 3u); }
 
@@ -987,6 +1000,15 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             for (int k = 0; k < 6; k++) buf[g][k] = *reinterpret_cast<const uint2*>(tab + off[k] + 8 * ring_slot(6 * g + k));
     };
     prime();
+    // LDS byte addresses of the lane's six table columns, held in VGPRs across the chunks (the
+    // compiler otherwise re-adds the ring base to each column offset in every chunk: 6 VALU per
+    // chunk; round 3 A/B -0.3 % soft, -0.4 % hard per 4,096-frame launch)
+    uint32_t tad[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        tad[k] = lds_addr(tab) + off[k];
+        asm volatile("" : "+v"(tad[k]));
+    }
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
@@ -1006,9 +1028,15 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         constexpr bool GSC = decltype(gtag)::value;
         constexpr bool LASTC = decltype(lasttag)::value;
         const int c0 = t0 / kChunk;
+#ifdef VTB_EXP_B128
         const uint2* ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
+#else
+        LdsCol ap[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) ap[k].a = tad[k];
+#endif
         uint32_t* dchunk = dec + ((t0 - lds_t0) >> 4) * 64 + widx;  // (LDS words; stream: this call's)
         // GS: byte offset of the lane's words (streaming: position in the survivor ring)
         const uint32_t gvo = 4u * (((STREAM ? t0 % sa.ring : t0) >> 4) * 64 + widx);
