@@ -331,6 +331,9 @@ def load_valu(workload_key):
 # SIMD (v_add_u32 / v_pk_min_u16 / DPP adds: tools/probes/isa_bench.hip, profiles/r01), at the
 # 2.4 GHz peak engine clock.
 VALU_PEAK_G = 256 * 4 * 2.4 / 4
+# The SIMD-32's full-rate issue (a wave64 instruction every 2 cycles, MI355X_MICROARCH.md:54),
+# reached only by the plain 32-bit ops with two or more waves per SIMD (profiles/r01/isa_bench*.txt)
+VALU_PEAK_2CYC_G = 256 * 4 * 2.4 / 2
 
 
 def stream_bench(args, dev, local, world):
@@ -654,6 +657,7 @@ def main():
         ach = valu["valu_wave_insts_per_launch"] / (kern_ms * 1e-3) / 1e9
         secondary.update({"achieved": round(ach, 2), "peak": VALU_PEAK_G, "unit": "G wave64-VALU-instr/s",
                           "frac": round(ach / VALU_PEAK_G, 4),
+                          "peak_2cycle": VALU_PEAK_2CYC_G, "frac_2cycle": round(ach / VALU_PEAK_2CYC_G, 4),
                           "valu_wave_insts_per_launch": valu["valu_wave_insts_per_launch"]})
 
     if rank != 0:
