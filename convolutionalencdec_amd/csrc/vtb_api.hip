@@ -313,6 +313,19 @@ hipError_t workspace_alloc(void** p, size_t bytes, hipStream_t stream) {
     return hipMallocFromPoolAsync(p, bytes, pool, stream);
 }
 
+int current_device_cus() {
+    static std::mutex mu;
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache[dev] == 0) {
+        int cus = 0;
+        cache[dev] = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 ? cus : 256;
+    }
+    return cache[dev];
+}
+
 int resident_per_cu(const void* kernel, size_t lds) {
     struct Entry {
         const void* k;

@@ -449,6 +449,32 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     const int T = info_bits / k + S, N = 1 << (k * S), E = 1 << k, R = (N + 63) / 64;
     if (in_stride < size_t(T) || out_stride < size_t((info_bits + 7) / 8)) return VTB_ERR_INVALID;
     if (frames == 0) return VTB_OK;
+    hipStream_t st = (hipStream_t)stream;
+    // k = 1, K = 7, rate 1/3, hard segments: the K=7 LDS pair kernel with a 16-column table
+    // (vtb_k7_lds.hip, k7_pair NB = 3).  Its butterfly takes the upper predecessor's branch
+    // metric as n - e (reference viterbiDecoderButterflyk1.c:104-107): the reference's own
+    // arithmetic for any generators, and the exact one when every generator taps both ends.
+    // Its exact metrics equal the reference's uint8 ones at n = 3 (the minimum grows by at most
+    // one per step, so nothing wraps: DESIGN.md §3, §4.7).  VTB_KERNEL=genk keeps this kernel.
+    if (k == 1 && K == 7 && n == 3 && !vtb::env_is("VTB_KERNEL", "genk")) {
+        bool ends = true;
+        for (int i = 0; i < n; i++) ends = ends && ((code->generators[i] >> (K - 1)) & 1u) && (code->generators[i] & 1u);
+        vtb::Launch la;
+        la.S = S, la.soft = 0, la.T = T, la.L = info_bits;
+        la.in = d_in, la.in_stride = in_stride, la.out = d_out, la.out_stride = out_stride;
+        la.frames = frames, la.stream = st, la.cus = vtb::current_device_cus();
+        uint32_t rg[3];
+        for (int i = 0; i < 3; i++) rg[i] = vtb::gen_rev(code->generators[i], K);
+        for (int j = 0; j < 32; j++) {  // label of butterfly j: the encoder on delay (j << 1) | 0 (reference :24-29)
+            uint32_t c = 0;
+            for (int i = 0; i < 3; i++) c |= uint32_t(__builtin_popcount((uint32_t(j) << 1) & rg[i]) & 1) << i;
+            la.symm[j] = uint8_t(c);
+        }
+        if ((u8 || ends) && vtb::k7_n3_supported(la)) {
+            const hipError_t e = vtb::launch_k7_lds_n3(la);
+            return e == hipSuccess ? VTB_OK : e == hipErrorOutOfMemory ? VTB_ERR_NOMEM : VTB_ERR_DEVICE;
+        }
+    }
     vtb::GenArgs a{};
     a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R, a.u8 = u8 ? 1 : 0;
     a.dbg = vtb::debug_flags();
@@ -461,7 +487,6 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     const bool gdec = dec_bytes > 32 * 1024;
     const vtb::GenLayout ly = vtb::gen_layout(N, E, T, info_bits, S, gdec);
     if (ly.total > 160 * 1024 || frames > 0x7fffffffu) return VTB_ERR_UNSUPPORTED;
-    hipStream_t st = (hipStream_t)stream;
     vtb::note_kernel("genk");
     const auto kern = [&](bool g) -> const void* {
         switch (k) {

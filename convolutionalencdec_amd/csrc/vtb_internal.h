@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 namespace vtb {
 
@@ -68,6 +69,15 @@ inline int debug_flags() {
 // launch otherwise).  0 if unknown.
 int resident_per_cu(const void* kernel, size_t lds);
 
+// Compute units of the calling thread's current device (cached per device; 256 if unknown).
+int current_device_cus();
+
+// getenv(name) equals value.
+inline bool env_is(const char* name, const char* value) {
+    const char* v = getenv(name);
+    return v && strcmp(v, value) == 0;
+}
+
 // Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
 // shape limits are reported through *_supported() beforehand.
 bool lds_path_supported(const Launch& a);
@@ -77,6 +87,9 @@ hipError_t launch_lds_path(const Launch& a);
 bool k7_lds_supported(const Launch& a);
 size_t k7_lds_bytes(const Launch& a);
 hipError_t launch_k7_lds(const Launch& a);
+// k = 1 rate-1/3 codes, hard input (a.symm: 3-bit butterfly labels), the K=7 LDS pair kernel
+bool k7_n3_supported(const Launch& a);
+hipError_t launch_k7_lds_n3(const Launch& a);
 
 // K=7, the same kernel with survivor words in a global workspace (vtb_k7_lds.hip): long
 // frames, and frames whose LDS survivors would cut the occupancy.

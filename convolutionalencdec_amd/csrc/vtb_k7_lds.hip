@@ -92,6 +92,14 @@ constexpr int kCol = 49;                   // 8-byte slots per table column (48 
 __host__ __device__ constexpr int ring_slot(int r) { return r; }
 #endif
 constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) columns
+// Rate 1/3 (NB = 3): 16 (label, R) columns of a 24-row ring (25 slots: the 16 columns of a row
+// in distinct bank pairs), refilled half a chunk at a time (k7_pair), so that the ring, 3.2 KB,
+// leaves 8 waves per CU at L = 1,024 like the rate-1/2 ring.
+template <int NB>
+constexpr int kColN = NB == 3 ? 25 : kCol;   // 8-byte slots per table column
+template <int NB>
+constexpr int kRowsN = NB == 3 ? 24 : kChunk;  // ring rows
+constexpr int ring_bytes(int NB) { return (2 << NB) * (NB == 3 ? kColN<3> : kCol) * 8; }
 #ifndef VTB_EXP_TBWARM
 #define VTB_EXP_TBWARM 48
 #endif
@@ -105,12 +113,15 @@ constexpr uint32_t kR1 = 0x10001u;
 // exact metric needs 14 bits); hard input, whose metrics stay below 128, keeps 256m + h
 // with 8 history bits (tie bit at t mod 8, clear and survivor byte every 8 steps, eight
 // decisions per traceback read).
-template <bool SOFT>
+// NB (k = 1 codes of rate 1/NB; 3 only for hard input, through vtb_genk_decode_device): the
+// spread bound and the start value scale with the largest branch metric NB Q.
+template <bool SOFT, int NB = 2>
 struct Hist {
+    static_assert(NB == 2 || (NB == 3 && !SOFT), "rate 1/3: hard input only");
     static constexpr int HB = SOFT ? 2 : 8;                  // history bits
     static constexpr uint32_t SC = 1u << HB;                 // metric scale
     static constexpr uint32_t MASK = (SC - 1) * 0x10001u;    // history bits of both frames
-    static constexpr uint32_t BIAS = SC * (SOFT ? 3060 : 12);  // renormalised location-0 metric (scaled)
+    static constexpr uint32_t BIAS = SC * (SOFT ? 3060 : 6 * NB);  // renormalised location-0 metric (scaled)
 };
 
 int tb_block(int T) {
@@ -135,11 +146,11 @@ __host__ __device__ constexpr int split_t1(int T, int warm = kSplitWarm) {
 }
 // LDS: [0, r0) table ring, later the decoded bytes of both frames; [r0, r0 + 16*Tpad)
 // survivor words.
-int region0(int T) {  // multiple of 256: the traceback edits survivor-word addresses in place
-    const int r = 8 * tb_block(T) > kRingBytes ? 8 * tb_block(T) : kRingBytes;
+int region0(int T, int NB = 2) {  // multiple of 256: the traceback edits survivor-word addresses in place
+    const int r = 8 * tb_block(T) > ring_bytes(NB) ? 8 * tb_block(T) : ring_bytes(NB);
     return (r + 255) / 256 * 256;
 }
-size_t lds_bytes(int T) { return (size_t)region0(T) + 16 * (size_t)t_pad(T); }
+size_t lds_bytes(int T, int NB = 2) { return (size_t)region0(T, NB) + 16 * (size_t)t_pad(T); }
 
 // Measurement only: phase timestamp k of this wave (Launch::tstamp, 8 u64 per wave).
 __device__ __forceinline__ void tstamp(const Launch& table, int k) {
@@ -692,12 +703,13 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
 // stream_traceback below).
 // Per phase: byte offset of the lane's (V, W) column in the table ring: its edge label c
 // and R = bit p of its location (the same for every frame pair of the wave).
+template <int NB = 2>
 __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[6], int lane) {
     const int loc = int(lane_of(uint32_t(lane)));
 #pragma unroll
     for (int ph = 0; ph < 6; ph++) {
         const int p = 5 - ph;
-        off[ph] = 8u * kCol * (table.symm[rotl6(loc & ~(1 << p), ph)] + 4u * ((loc >> p) & 1u));
+        off[ph] = 8u * kColN<NB> * (table.symm[rotl6(loc & ~(1 << p), ph)] + (1u << NB) * ((loc >> p) & 1u));
     }
 }
 
@@ -767,7 +779,8 @@ struct SegArgs {
 // table.fail_list (the frames a persistent split launch could not decode split), `frames` = the
 // list's count.  SPLIT with LOOP (the persistent split kernel): a split pass that does not
 // converge appends the frame to table.fail_list instead of decoding it again in the wave.
-template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT, bool SEG = false, bool LIST = false>
+// NB: coded bits per step (2; 3 for the hard rate-1/3 pair kernel, k7_lds_n3)
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT, bool SEG = false, bool LIST = false, int NB = 2>
 __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int Tpad, int tbb, int r0, size_t frames,
                                         int dbg, const Launch& table, uint8_t* __restrict__ ws, size_t ws_wave,
@@ -776,10 +789,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                                         const SegArgs* sgp = nullptr, uint32_t* seg_out = nullptr) {
     static_assert(!SEG || (SPLIT && !GS && !STREAM && !LOOP), "SEG runs the split pair on LDS survivors");
     static_assert(!LIST || (GS && LOOP && !SPLIT && !STREAM), "the list kernel is the persistent global variant");
+    static_assert(NB == 2 || (!SOFT && !GS && !STREAM && !SPLIT && !SEG && !LIST), "rate 1/3: the hard LDS pair kernel only");
 
     constexpr uint32_t Q = SOFT ? 255 : 1;
-    constexpr uint32_t INIT = 12 * Q + 1;  // start metric of states != 0 (see header)
-    using H = Hist<SOFT>;
+    constexpr int NL = 1 << NB;                 // edge labels
+    constexpr uint32_t INIT = 6 * NB * Q + 1;  // start metric of states != 0: above six steps of the largest branch metric (see header)
+    using H = Hist<SOFT, NB>;
     extern __shared__ uint4 smem4[];
     const int wv = SEG ? int(threadIdx.x >> 6) : 0;  // SEG: wave of the workgroup
     uint8_t* smem = reinterpret_cast<uint8_t*>(smem4) + (SEG ? wv * sgp->seg_bytes : 0);
@@ -874,7 +889,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // in both halves).  Branch-free, so the compiler can interleave it with ACS steps.
     // first: no survivor stores outstanding.  In the loop (GS) one survivor-word store (step
     // 15 of the chunk) was issued after the loads; vmcnt retires in issue order.
-    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4], bool first) {
+    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[NL], uint32_t (&et)[NL], bool first) {
 #ifdef VTB_EXP_RAWNOWAIT
         ra = lane * 0x0101u, rb = lane * 0x0303u;  // measurement only: no wait for the loads
 #else
@@ -888,9 +903,10 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #endif
         // packed [frame A, frame B] received values of coded bits 0 and 1, times four
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
-        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
+        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u), q2 = 0;
         if constexpr (!SOFT) {
             q1 = (q0 >> 1) & kR1;
+            if constexpr (NB == 3) q2 = (q0 >> 2) & kR1;  // (bits above coded bit NB-1 are ignored)
             q0 &= kR1;
         }
         q0 <<= H::HB;
@@ -898,9 +914,18 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         // 4e of labels 0..3 (bit 0 of a label <-> coded bit 0); halves never borrow
         constexpr uint32_t QQ = H::SC * Q * kR1;
         e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
+        if constexpr (NB == 3) {
+            // labels 4..7 set coded bit 2: e(c) = e(c & 3) + (c & 4 ? Q - q2 : q2); e(~c) = 3Q - e(c)
+            q2 <<= H::HB;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                e[4 + k] = e[k] + (QQ - q2);
+                e[k] += q2;
+            }
+        }
         const uint32_t tie = (1u << (srow & (H::HB - 1))) * kR1;
 #pragma unroll
-        for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
+        for (int k = 0; k < NL; k++) et[k] = e[k] + tie;
     };
     // Column k = c + 4R of the ring holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
     // (V, W) of a slot from two unrelated VGPRs by ds_write2_b32 (a ds_write_b64 would need
@@ -909,8 +934,40 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const uint32_t wbase0 = uint32_t(SEG ? wv * sgp->seg_bytes : 0) + 8u * uint32_t(ring_slot(srow)), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
     // PADCHK: the chunk may hold padding rows (only the chunk containing step T; the ACS
     // loop is split so that the check stays out of its other iterations).
-    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4], auto padchk) {
+    auto stage_write = [&](int c, const uint32_t (&e)[NL], const uint32_t (&et)[NL], auto padchk, int half = 0) {
         constexpr bool PADCHK = decltype(padchk)::value;
+        if constexpr (NB == 3) {
+            // rows [24 half, 24 half + 24) of chunk c into the 24-row ring (slot = row mod 24);
+            // 16 columns k = c + 8R: (V, W) = (4e(c) + R tie, 4e(7 - c) + (1 - R) tie), the
+            // complement's metric 3Q - e(c) as the reference's n - e (viterbiDecoderButterflyk1.c:104-107).
+            // (V, W) by ds_write2_b32 from two unrelated VGPRs, five columns per base address
+            // (offsets below 256 dwords)
+            constexpr int KC = kColN<3>;
+            if (srow / 24 == half) {
+                const uint32_t b0 = uint32_t(lds_addr(tab)) + 8u * uint32_t(srow % 24);
+                const uint32_t bs[4] = {b0, b0 + 40u * KC, b0 + 80u * KC, b0 + 120u * KC};
+#define VTB_W3(k, v, w)                                                                                 \
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(bs[(k) / 5]), "v"(v), "v"(w),   \
+                 "i"(2 * KC * ((k) % 5)), "i"(2 * KC * ((k) % 5) + 1) : "memory");
+                VTB_W3(0, e[0], et[7]) VTB_W3(1, e[1], et[6]) VTB_W3(2, e[2], et[5]) VTB_W3(3, e[3], et[4])
+                VTB_W3(4, e[4], et[3]) VTB_W3(5, e[5], et[2]) VTB_W3(6, e[6], et[1]) VTB_W3(7, e[7], et[0])
+                VTB_W3(8, et[0], e[7]) VTB_W3(9, et[1], e[6]) VTB_W3(10, et[2], e[5]) VTB_W3(11, et[3], e[4])
+                VTB_W3(12, et[4], e[3]) VTB_W3(13, et[5], e[2]) VTB_W3(14, et[6], e[1]) VTB_W3(15, et[7], e[0])
+#undef VTB_W3
+                if (PADCHK && c * kChunk + srow >= T) {  // padding rows: own-keeping (below), rare
+                    uint2* col = reinterpret_cast<uint2*>(tab) + (srow % 24);  // column k at col[KC * k]
+                    constexpr uint32_t PADW = H::SC * INIT * kR1;
+                    const uint32_t tie = et[0] - e[0];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        col[k * KC] = make_uint2(0u, PADW + tie);
+                        col[(8 + k) * KC] = make_uint2(tie, PADW);
+                    }
+                }
+            }
+            asm volatile("" ::: "memory");  // (ordered against the table reads)
+            return;
+        }
         uint2* col = reinterpret_cast<uint2*>(tab) + ring_slot(srow);  // column k at col[kCol * k]
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
@@ -924,7 +981,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             // there, as below
             const int tr = c * kChunk + srow;
             if (PADCHK && (tr >= Ta || tr >= Tb)) {
-                constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
+                constexpr uint32_t PADW = H::SC * INIT * kR1;
                 const uint32_t keep = (tr >= Ta ? 0u : 0xFFFFu) | (tr >= Tb ? 0u : 0xFFFF0000u);
                 const uint32_t tie = et[0] - e[0];
 #pragma unroll
@@ -936,7 +993,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         } else if (SPLIT && sp) {
             // split pass: padding rows of frame B only (step >= Tb); frame A's half is real
             if (PADCHK && c * kChunk + srow >= Tb) {
-                constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1, LO = 0xFFFFu, HI = 0xFFFF0000u;
+                constexpr uint32_t PADW = H::SC * INIT * kR1, LO = 0xFFFFu, HI = 0xFFFF0000u;
                 const uint32_t tie = et[0] - e[0];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -945,7 +1002,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 }
             }
         } else if (PADCHK && (c + 1) * kChunk > T && c * kChunk + srow >= T) {  // padding rows
-            constexpr uint32_t PADW = H::SC * (12 * Q + 1) * kR1;
+            constexpr uint32_t PADW = H::SC * INIT * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -954,8 +1011,16 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             }
         }
     };
+    // staged row values of the next chunk (computed at group 3, written at group 8 - AH; NB = 3:
+    // its second half at group 1 of that chunk)
+    uint32_t se[NL], set[NL];
     auto stage = [&](int c, uint32_t ra, uint32_t rb) {
-        uint32_t e[4], et[4];
+        if constexpr (NB == 3) {  // the chunk's first half now, its second at its group 1 (from se/set)
+            stage_compute(ra, rb, se, set, true);
+            stage_write(c, se, set, std::true_type{}, 0);
+            return;
+        }
+        uint32_t e[NL], et[NL];
         stage_compute(ra, rb, e, et, true);
         stage_write(c, e, et, std::true_type{});
     };
@@ -1011,7 +1076,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     }
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
-    uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0}, se[4], set[4];
+    uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0};
 #ifdef VTB_EXP_SGMASK
     uint32_t clr_mask;
     asm volatile("s_mov_b32 %0, %1" : "=s"(clr_mask) : "i"(~H::MASK));
@@ -1098,6 +1163,9 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         if ((G) == 8 - AH && VTB_EXP_STAGE && !LASTC) { /* all rows of this chunk are in registers */ \
             stage_write(c0 + 1, se, set, padtag);                                                 \
         }                                                                                         \
+        if (NB == 3 && (G) == 1 && VTB_EXP_STAGE) { /* rows 24-47 of this chunk: rows 0-23 are read */ \
+            stage_write(c0, se, set, std::true_type{}, 1);                                       \
+        }                                                                                         \
         uint2* cur = buf[(G) & 3];                                                                \
         /* table reads AH groups ahead, issued after the two permlane steps */                     \
         VTB_STEP(6 * (G) + 0, 0) VTB_STEP(6 * (G) + 1, 1)                                         \
@@ -1119,13 +1187,13 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #else
 #define VTB_RD(G, k)                                                                              \
     if (((G) & 1) == 0) {                                                                         \
-        buf[((G) + 2) & 3][k] = ap[k][(6 * ((G) + 2) + (k)) % kChunk];                            \
-        buf[((G) + 3) & 3][k] = ap[k][(6 * ((G) + 3) + (k)) % kChunk];                            \
+        buf[((G) + 2) & 3][k] = ap[k][(6 * ((G) + 2) + (k)) % kChunk % kRowsN<NB>];               \
+        buf[((G) + 3) & 3][k] = ap[k][(6 * ((G) + 3) + (k)) % kChunk % kRowsN<NB>];               \
     }
 #endif
 #else
 #define VTB_RD(G, k)                                                                              \
-    buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk], buf[(G) & 3][k]);
+    buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk % kRowsN<NB>], buf[(G) & 3][k]);
 #endif
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
@@ -1413,7 +1481,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // the dispatcher refilling freed slots unevenly).  !LOOP: one wave per pair, for batches the
 // CUs hold in one round and for the streaming decoder (the loop's extra live state costs
 // ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
-template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false, bool LIST = false>
+template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false, bool LIST = false, int NB = 2>
 #ifdef VTB_EXP_WPE
 #define VTB_K7_WPE __attribute__((amdgpu_waves_per_eu(1, VTB_EXP_WPE)))
 #else
@@ -1434,15 +1502,16 @@ __global__ __launch_bounds__(64) VTB_K7_WPE void k7_lds_kernel(const uint8_t* __
         tstamp(table, 0);
         clk0 = __builtin_amdgcn_s_memtime();
     }
-    column_offsets(table, off, threadIdx.x);
+    column_offsets<NB>(table, off, threadIdx.x);
     if constexpr (!LOOP) {
-        k7_pair<SOFT, GS, STREAM, false, SPLIT>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames, dbg, table, ws,
-                                         ws_wave, sa, blockIdx.x, blockIdx.x, false, pairs, pra, prb, off);
+        k7_pair<SOFT, GS, STREAM, false, SPLIT, false, false, NB>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0,
+                                                                  frames, dbg, table, ws, ws_wave, sa, blockIdx.x,
+                                                                  blockIdx.x, false, pairs, pra, prb, off);
     } else {
         // units: frame pairs, or (SPLIT) frames; every wave leaves the loop when the units run out
         const size_t units = SPLIT ? frames : pairs;
         for (size_t wp = blockIdx.x; wp < units; wp += gridDim.x) {
-            k7_pair<SOFT, GS, STREAM, true, SPLIT, false, LIST>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames,
+            k7_pair<SOFT, GS, STREAM, true, SPLIT, false, LIST, NB>(in, in_stride, out, out_stride, T, L, Tpad, tbb, r0, frames,
                                                                 dbg, table, ws, ws_wave, sa, wp, blockIdx.x,
                                                                 !GS && wp != blockIdx.x, wp + gridDim.x, pra, prb, off);
             __syncthreads();  // LDS of this pair (decoded bytes) before the next pair's table ring
@@ -1764,6 +1833,34 @@ bool k7_lds_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_byt
 size_t k7_lds_bytes(const Launch& a) { return lds_bytes(a.T); }
 
 hipError_t launch_k7_lds(const Launch& a) { return launch_k7<false>(a); }
+
+// Rate 1/3 (k = 1, n = 3), hard input: the LDS pair kernel with a 16-column branch-metric ring
+// (k7_pair NB = 3), one round or persistent over the frame pairs.  a.symm holds the 3-bit labels.
+bool k7_n3_supported(const Launch& a) { return a.S == 6 && !a.soft && a.T > a.S && lds_bytes(a.T, 3) <= 160 * 1024; }
+
+hipError_t launch_k7_lds_n3(const Launch& a) {
+    if (a.frames == 0) return hipSuccess;
+    if (!k7_n3_supported(a)) return hipErrorInvalidValue;
+    const size_t lds = lds_bytes(a.T, 3), pairs = (a.frames + 1) / 2;
+    auto once = k7_lds_kernel<false, false, false, false, false, false, 3>;
+    auto loop = k7_lds_kernel<false, false, false, true, false, false, 3>;
+    for (auto k : {once, loop}) {
+        if (lds > 64 * 1024) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+            if (e != hipSuccess) return e;
+        }
+    }
+    const int per_cu = resident_per_cu(reinterpret_cast<const void*>(loop), lds);
+    size_t grid = pairs;
+    if (per_cu > 0 && size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1) < grid) grid = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
+    const bool lp = grid < pairs;
+    note_kernel(lp ? "k7_lds_n3_loop" : "k7_lds_n3");
+    hipLaunchKernelGGL(lp ? loop : once, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T, 3), a.frames, debug_flags(), a,
+                       static_cast<uint8_t*>(nullptr), size_t(0), StreamArgs());
+    return hipGetLastError();
+}
 
 bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T, a.soft) <= 160 * 1024; }
 

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     for (int t = top - 1; active && t >= lo; t--) st = pred(st, t);
     unsigned fin = st;
     bool fixed = !active || start == T;
-    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << G) - 1)) << (fi * G);
+    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
     for (int round = 0; round <= G; round++) {
         const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
         const bool ok = fixed || s_top == sf;
