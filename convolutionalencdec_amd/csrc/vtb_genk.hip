@@ -450,13 +450,13 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     if (in_stride < size_t(T) || out_stride < size_t((info_bits + 7) / 8)) return VTB_ERR_INVALID;
     if (frames == 0) return VTB_OK;
     hipStream_t st = (hipStream_t)stream;
-    // k = 1, K = 7, rate 1/3, hard segments: the K=7 LDS pair kernel with a 16-column table
-    // (vtb_k7_lds.hip, k7_pair NB = 3).  Its butterfly takes the upper predecessor's branch
+    // k = 1, K = 7 or 9, rate 1/3, hard segments: the K=7 LDS pair kernel / the K=9 frame kernel
+    // with a 16-column table (vtb_k7_lds.hip k7_pair NB = 3, vtb_k9.hip k9_pair NB = 3).  Its butterfly takes the upper predecessor's branch
     // metric as n - e (reference viterbiDecoderButterflyk1.c:104-107): the reference's own
     // arithmetic for any generators, and the exact one when every generator taps both ends.
     // Its exact metrics equal the reference's uint8 ones at n = 3 (the minimum grows by at most
     // one per step, so nothing wraps: DESIGN.md §3, §4.7).  VTB_KERNEL=genk keeps this kernel.
-    if (k == 1 && K == 7 && n == 3 && !vtb::env_is("VTB_KERNEL", "genk")) {
+    if (k == 1 && (K == 7 || K == 9) && n == 3 && !vtb::env_is("VTB_KERNEL", "genk")) {
         bool ends = true;
         for (int i = 0; i < n; i++) ends = ends && ((code->generators[i] >> (K - 1)) & 1u) && (code->generators[i] & 1u);
         vtb::Launch la;
@@ -465,14 +465,24 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
         la.frames = frames, la.stream = st, la.cus = vtb::current_device_cus();
         uint32_t rg[3];
         for (int i = 0; i < 3; i++) rg[i] = vtb::gen_rev(code->generators[i], K);
-        for (int j = 0; j < 32; j++) {  // label of butterfly j: the encoder on delay (j << 1) | 0 (reference :24-29)
+        for (int j = 0; j < (1 << (K - 2)); j++) {  // label of butterfly j: the encoder on delay (j << 1) | 0 (reference :24-29)
             uint32_t c = 0;
             for (int i = 0; i < 3; i++) c |= uint32_t(__builtin_popcount((uint32_t(j) << 1) & rg[i]) & 1) << i;
             la.symm[j] = uint8_t(c);
         }
-        if ((u8 || ends) && vtb::k7_n3_supported(la)) {
+        if ((u8 || ends) && K == 7 && vtb::k7_n3_supported(la)) {
             const hipError_t e = vtb::launch_k7_lds_n3(la);
             return e == hipSuccess ? VTB_OK : e == hipErrorOutOfMemory ? VTB_ERR_NOMEM : VTB_ERR_DEVICE;
+        }
+        // K = 9 (the K=9 frame kernel, survivors in a workspace from the stream's pool)
+        if ((u8 || ends) && K == 9 && vtb::k9_n3_supported(la)) {
+            void* ws = nullptr;
+            if (vtb::workspace_alloc(&ws, vtb::k9_n3_workspace_bytes(la), st) != hipSuccess) return VTB_ERR_NOMEM;
+            la.ws = ws;
+            const hipError_t e = vtb::launch_k9_n3(la);
+            const bool freed = vtb::workspace_free(ws, st) == hipSuccess;
+            if (e != hipSuccess) return e == hipErrorOutOfMemory ? VTB_ERR_NOMEM : VTB_ERR_DEVICE;
+            return freed ? VTB_OK : VTB_ERR_DEVICE;
         }
     }
     vtb::GenArgs a{};

@@ -161,6 +161,10 @@ hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t
 bool k9_supported(const Launch& a);
 size_t k9_workspace_bytes(const Launch& a);
 hipError_t launch_k9(const Launch& a);
+// k = 1 rate-1/3 codes, hard input (a.symm: 3-bit butterfly labels), the K=9 frame kernel
+bool k9_n3_supported(const Launch& a);
+size_t k9_n3_workspace_bytes(const Launch& a);
+hipError_t launch_k9_n3(const Launch& a);
 
 // True if device `dev` is a gfx950 (answered once per device: the property query costs ~1 ms).
 bool device_is_gfx950(int dev);

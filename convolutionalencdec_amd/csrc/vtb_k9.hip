@@ -89,8 +89,10 @@ int tb_block(int Tq) {
     return (per + 47) / 48 * 48;
 }
 int t_pad(int Tq) { return (Tq + kCh - 1) / kCh * kCh; }
-int region0(int Tq) {  // table ring, later the decoded bytes of both frames
-    const int r = 8 * tb_block(Tq) > kRingBytes ? 8 * tb_block(Tq) : kRingBytes;
+// NB = 3 (k = 1 rate 1/3, hard input, vtb_genk_decode_device): 16 (label, R) columns
+constexpr int ring_bytes(int NB) { return (2 << NB) * kCol * 8; }
+int region0(int Tq, int NB = 2) {  // table ring, later the decoded bytes of both frames
+    const int r = 8 * tb_block(Tq) > ring_bytes(NB) ? 8 * tb_block(Tq) : ring_bytes(NB);
     return (r + 255) / 256 * 256;
 }
 size_t ws_wave_bytes(int Tq) { return (size_t)kColBytes * (t_pad(Tq) / 16); }
@@ -426,6 +428,7 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
 
 // Per register and phase: byte offset of the (V, W) column (edge label c of the butterfly's
 // upper state, R = bit p of the location); the same for every frame pair of the wave.
+template <int NB = 2>
 __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&off)[4][8], int lane) {
     const uint32_t lam = lane_of(uint32_t(lane));
 #pragma unroll
@@ -433,7 +436,7 @@ __device__ __forceinline__ void column_offsets(const Launch& table, uint32_t (&o
 #pragma unroll
         for (int ph = 0; ph < 8; ph++) {
             const int l = r * 64 + int(lam), p = 7 - ph;
-            off[r][ph] = 8u * kCol * (table.symm[rotl8(l & ~(1 << p), ph)] + 4u * ((l >> p) & 1u));
+            off[r][ph] = 8u * kCol * (table.symm[rotl8(l & ~(1 << p), ph)] + (1u << NB) * ((l >> p) & 1u));
         }
 }
 
@@ -453,15 +456,19 @@ struct Seg9 {
     int in_lds = 0;              // LDS byte offset of the staged frame
 };
 
-template <bool SOFT, bool STREAM = false, bool SEG = false>
+// NB: coded bits per step (2; 3 for the hard rate-1/3 frame kernel, launch_k9_n3)
+template <bool SOFT, bool STREAM = false, bool SEG = false, int NB = 2>
 __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
                                         size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
                                         size_t frames, int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t wp,
                                         size_t slot, const uint32_t (&off)[4][8], const StreamArgs& sa = StreamArgs(),
                                         const Seg9* sg = nullptr, uint32_t* seg_out = nullptr) {
+    static_assert(NB == 2 || (!SOFT && !STREAM && !SEG), "rate 1/3: the hard frame kernel only");
     constexpr uint32_t Q = SOFT ? 255 : 1;
+    constexpr int NL = 1 << NB;  // edge labels
     using H = Hist<SOFT>;
-    constexpr uint32_t B4 = H::SC * 16 * Q;  // renormalised metric of location 0 (scaled)
+    // renormalised metric of location 0 (scaled): the metric spread bound n Q S (n = NB, S = 8)
+    constexpr uint32_t B4 = H::SC * 8 * NB * Q;
     extern __shared__ uint4 smem4[];
     const int wv = SEG ? int(threadIdx.x >> 6) : 0;
     uint8_t* tab = reinterpret_cast<uint8_t*>(smem4) + (SEG ? wv * sg->ring_bytes : 0);
@@ -517,31 +524,53 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                          : "=&v"(ra), "=&v"(rb) : "v"(uint32_t(t)), "s"(baseA), "s"(baseB));
         }
     };
-    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[4], uint32_t (&et)[4]) {
+    auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[NL], uint32_t (&et)[NL]) {
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
-        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
+        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u), q2 = 0;
         if constexpr (!SOFT) {
             q1 = (q0 >> 1) & kR1;
+            if constexpr (NB == 3) q2 = (q0 >> 2) & kR1;  // (bits above coded bit NB-1 are ignored)
             q0 &= kR1;
         }
         q0 <<= H::HB;
         q1 <<= H::HB;
         constexpr uint32_t QQ = H::SC * Q * kR1;
         e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
+        if constexpr (NB == 3) {  // labels 4..7 set coded bit 2 (vtb_k7_lds.hip stage_compute)
+            q2 <<= H::HB;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                e[4 + k] = e[k] + (QQ - q2);
+                e[k] += q2;
+            }
+        }
         const uint32_t tie = (1u << (srow & (H::HB - 1))) * kR1;
 #pragma unroll
-        for (int k = 0; k < 4; k++) et[k] = e[k] + tie;
+        for (int k = 0; k < NL; k++) et[k] = e[k] + tie;
     };
     // Column k = c + 4R holds (V, W) = (4e(c) + R tie, 4e(~c) + (1 - R) tie).
     const uint32_t wbase0 = uint32_t(SEG ? wv * sg->ring_bytes : 0) + 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol,
                    wbase2 = wbase0 + 48u * kCol;
-    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
+    auto stage_write = [&](int c, const uint32_t (&e)[NL], const uint32_t (&et)[NL]) {
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
                  "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
-        VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
-        VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
-        VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+        if constexpr (NB == 3) {
+            // 16 columns k = c + 8R: (V, W) = (e(c) + R tie, e(7 - c) + (1 - R) tie), the
+            // complement's metric 3Q - e(c) as the reference's n - e (viterbiDecoderButterflyk1.c:104-107);
+            // three columns per base address (offsets below 256 dwords)
+            const uint32_t wb3 = wbase2 + 24u * kCol, wb4 = wb3 + 24u * kCol, wb5 = wb4 + 24u * kCol;
+            VTB_W2(wbase0, 0, e[0], et[7]) VTB_W2(wbase0, 1, e[1], et[6]) VTB_W2(wbase0, 2, e[2], et[5])
+            VTB_W2(wbase1, 3, e[3], et[4]) VTB_W2(wbase1, 4, e[4], et[3]) VTB_W2(wbase1, 5, e[5], et[2])
+            VTB_W2(wbase2, 6, e[6], et[1]) VTB_W2(wbase2, 7, e[7], et[0]) VTB_W2(wbase2, 8, et[0], e[7])
+            VTB_W2(wb3, 9, et[1], e[6]) VTB_W2(wb3, 10, et[2], e[5]) VTB_W2(wb3, 11, et[3], e[4])
+            VTB_W2(wb4, 12, et[4], e[3]) VTB_W2(wb4, 13, et[5], e[2]) VTB_W2(wb4, 14, et[6], e[1])
+            VTB_W2(wb5, 15, et[7], e[0])
+        } else {
+            VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
+            VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
+            VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+        }
 #undef VTB_W2
         // Own-keeping rows: the start step of odd T; for hard input also the padding steps
         // past Tq (W = the metric spread nQS + 1 keeps every survivor at its own location,
@@ -567,12 +596,12 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         const bool pad_row = !SOFT && (c + 1) * kCh > Tq && c * kCh + srow >= Tq;
         if ((c == 0 && srow < delta) || pad_row) {
             uint2* col = reinterpret_cast<uint2*>(tab) + srow;
-            constexpr uint32_t PADW = H::SC * ((SOFT ? 2 : 16) * Q + 1) * kR1;
+            constexpr uint32_t PADW = H::SC * ((SOFT ? 2 : 8 * NB) * Q + 1) * kR1;
             const uint32_t tie = et[0] - e[0];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < NL; k++) {
                 col[k * kCol] = make_uint2(0u, PADW + tie);
-                col[(4 + k) * kCol] = make_uint2(tie, PADW);
+                col[(NL + k) * kCol] = make_uint2(tie, PADW);
             }
         }
     };
@@ -592,7 +621,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     }
     uint32_t ra, rb;
     if (!STREAM || Tpad > tbeg) {
-        uint32_t e[4], et[4];
+        uint32_t e[NL], et[NL];
         load_raw(tbeg / kCh, ra, rb);
         if constexpr (SEG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
         else asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
@@ -606,7 +635,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         for (int r = 0; r < 4; r++) buf[s][r] = *reinterpret_cast<const uint2*>(tab + off[r][s] + 8 * s);
 
     const uint32_t wlane = 4u * rev6(lam);  // survivor word byte offset of the lane within a column
-    uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[4], set[4], msave[4] = {0, 0, 0, 0};
+    uint32_t dd = 0, m_prev[4] = {0, 0, 0, 0}, pw[4][4] = {}, se[NL], set[NL], msave[4] = {0, 0, 0, 0};
     const int tacs = (dbg & 2) ? 0 : SEG ? sg->n : Tpad;
     // STREAM, soft, last call with odd T: the window of step T - 1 (the last real step, even)
     // also holds padding step T, whose ACS runs on clamped input; the metrics right after step
@@ -1017,25 +1046,25 @@ __global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__
 
 // LOOP: persistent over frame pairs (as vtb_k7_lds.hip), wave b decodes pairs b, b + grid, ...;
 // !LOOP: one wave per pair, for batches the CUs hold in one round (fewer live registers).
-template <bool SOFT, bool LOOP, bool STREAM = false>
+template <bool SOFT, bool LOOP, bool STREAM = false, int NB = 2>
 __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                 uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
                                                 int Tq, int Tpad, int tbb, size_t frames, int dbg, Launch table,
                                                 uint8_t* __restrict__ ws, size_t ws_wave, StreamArgs sa = StreamArgs()) {
     static_assert(!(STREAM && LOOP), "streaming calls keep per-pair state: one wave per pair");
     uint32_t off[4][8];
-    column_offsets(table, off, threadIdx.x);
+    column_offsets<NB>(table, off, threadIdx.x);
     if constexpr (STREAM) {
         k9_pair<SOFT, true>(in, in_stride, out, out_stride, T, L, 0, T, Tpad, 0, frames, dbg, ws, ws_wave, blockIdx.x,
                             blockIdx.x, off, sa);
     } else if constexpr (!LOOP) {
-        k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, blockIdx.x,
-                      blockIdx.x, off);
+        k9_pair<SOFT, false, false, NB>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws,
+                                        ws_wave, blockIdx.x, blockIdx.x, off);
     } else {
         const size_t pairs = (frames + 1) / 2;
         for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
-            k9_pair<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws, ws_wave, wp,
-                          blockIdx.x, off);
+            k9_pair<SOFT, false, false, NB>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws,
+                                            ws_wave, wp, blockIdx.x, off);
             __syncthreads();  // LDS (decoded bytes) before the next pair's table ring
         }
     }
@@ -1043,12 +1072,12 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
 
 // Grid: the frame pairs, at most what the CUs hold at once and at most 1 GiB of survivor
 // slots (one per wave).
-size_t grid_waves(const Launch& a, int Tq) {
+size_t grid_waves(const Launch& a, int Tq, int NB = 2) {
     const size_t pairs = (a.frames + 1) / 2;
     size_t grid = pairs;
-    auto kern = a.soft ? k9_kernel<true, true> : k9_kernel<false, true>;
+    auto kern = NB == 3 ? k9_kernel<false, true, false, 3> : a.soft ? k9_kernel<true, true> : k9_kernel<false, true>;
     const int per_cu =
-        (debug_flags() & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq));
+        (debug_flags() & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq, NB));
     if (per_cu > 0) {
         const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
         if (resident < grid) grid = resident;
@@ -1152,6 +1181,35 @@ hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s) {
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), (size_t)kRingBytes, a.stream, a.in, a.in_stride, a.out,
                        a.out_stride, a.T, a.L, 0, a.T, s.t_end, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws),
                        size_t(kColBytes) / 16 * size_t(s.ring), s);
+    return hipGetLastError();
+}
+
+// k = 1 rate 1/3, hard input (a.symm: 3-bit butterfly labels): the K=9 frame kernel with a
+// 16-column branch-metric table (k9_pair NB = 3); survivors in a.ws (k9_n3_workspace_bytes).
+bool k9_n3_supported(const Launch& a) {
+    return a.S == 8 && !a.soft && a.T > a.S && (size_t)region0(a.T + (a.T & 1), 3) <= 160 * 1024;
+}
+size_t k9_n3_workspace_bytes(const Launch& a) {
+    const int Tq = a.T + (a.T & 1);
+    return grid_waves(a, Tq, 3) * ws_wave_bytes(Tq);
+}
+hipError_t launch_k9_n3(const Launch& a) {
+    if (a.frames == 0) return hipSuccess;
+    if (!a.ws || !k9_n3_supported(a)) return hipErrorInvalidValue;
+    const int delta = a.T & 1, Tq = a.T + delta;
+    const size_t lds = (size_t)region0(Tq, 3);
+    const size_t grid = grid_waves(a, Tq, 3);
+    const bool lp = grid < (a.frames + 1) / 2;
+    auto kern = lp ? k9_kernel<false, true, false, 3> : k9_kernel<false, false, false, 3>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+    }
+    note_kernel(lp ? "k9_n3_loop" : "k9_n3");
+    hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
+                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
+                       static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq), StreamArgs());
     return hipGetLastError();
 }
 

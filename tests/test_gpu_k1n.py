@@ -98,9 +98,9 @@ def test_reference_u8_mode_vs_oracle(orc, name, L):
             assert (got == unc).all()
 
 
-# ---- K=7 rate 1/3 on the K=7 LDS pair kernel (k7_pair NB = 3) ----
+# ---- K=7 / K=9 rate 1/3 on the K=7 LDS pair kernel / the K=9 frame kernel (NB = 3) ----
 
-K7N3 = K1N_PARAMS["k7n3"]
+N3 = {7: (K1N_PARAMS["k7n3"][1], "k7_lds_n3"), 9: (K1N_PARAMS["k9n3"][1], "k9_n3")}
 
 
 def genk_device_kernel(K, g, rx, L, flags, monkeypatch=None, force_genk=False):
@@ -115,59 +115,64 @@ def genk_device_kernel(K, g, rx, L, flags, monkeypatch=None, force_genk=False):
             monkeypatch.delenv("VTB_KERNEL")
 
 
+@pytest.mark.parametrize("K", [7, 9])
 @pytest.mark.parametrize("L", [1, 13, 64, 1001, 1024, 2048, 3000])
-def test_k7n3_fast_kernel_vs_oracle(orc, L):
-    """Reference arithmetic (U8 flag) and exact metrics both take the K=7 pair kernel and equal
-    the oracle's restatements bit for bit, garbage high bits included."""
-    K, g = K7N3
+def test_n3_fast_kernel_vs_oracle(orc, K, L):
+    """Reference arithmetic (U8 flag) and exact metrics both take the fast kernel and equal the
+    oracle's restatements bit for bit, garbage high bits included (odd and even T at K = 9)."""
+    g, kname = N3[K]
+    F = 37 if K == 7 else 21
     for p, seed in ((0.0, 11), (0.04, 12), (0.09, 13), (0.5, 14)):
         if L % 8 == 0:
-            unc, rx = k1n_frames(orc, K, g, L, 37, p, seed + L, garbage=(p == 0.04))
+            unc, rx = k1n_frames(orc, K, g, L, F, p, seed + L, garbage=(p == 0.04))
         else:
-            unc, rx = None, np.random.default_rng(seed + 5 * L).integers(0, 256, (37, L + K - 1), dtype=np.uint8)
+            unc, rx = None, np.random.default_rng(seed + 5 * L).integers(0, 256, (F, L + K - 1), dtype=np.uint8)
         got, kern = genk_device_kernel(K, g, rx, L, native.VTB_GENK_K1_REFERENCE_U8)
-        assert kern == "k7_lds_n3", kern
-        assert (got == orc.k1n_decode(K, g, rx, L)).all(), (L, p)
+        assert kern == kname, kern
+        assert (got == orc.k1n_decode(K, g, rx, L)).all(), (K, L, p)
         exact, kern = genk_device_kernel(K, g, rx, L, 0)
-        assert kern == "k7_lds_n3", kern
-        assert (exact == orc.genk_decode(1, K, g, rx, L)).all(), (L, p)
+        assert kern == kname, kern
+        assert (exact == orc.genk_decode(1, K, g, rx, L)).all(), (K, L, p)
         if unc is not None and p == 0.0:
             assert (got == unc).all()
 
 
-@pytest.mark.parametrize("g", [(0o133, 0o171, 0o165), (0o117, 0o127, 0o155), (0o132, 0o171, 0o165), (0o133, 0o070, 0o165)])
-def test_k7n3_generators(orc, g, monkeypatch):
+@pytest.mark.parametrize("K,g", [(7, (0o133, 0o171, 0o165)), (7, (0o117, 0o127, 0o155)), (7, (0o132, 0o171, 0o165)),
+                                 (7, (0o133, 0o070, 0o165)), (9, (0o557, 0o663, 0o711)), (9, (0o556, 0o663, 0o711))])
+def test_n3_generators(orc, K, g, monkeypatch):
     """Any generator set in the reference's arithmetic (the upper predecessor's metric n - e, whatever
     the taps: viterbiDecoderButterflyk1.c:104-107) on the fast kernel; exact metrics stay on the
     general kernel unless every generator taps both ends (n - e is then the true Hamming metric)."""
-    K, L = 7, 1024
+    kname = N3[K][1]
+    L = 1024
     unc, rx = k1n_frames(orc, K, g, L, 64, 0.07, 21)
     got, kern = genk_device_kernel(K, g, rx, L, native.VTB_GENK_K1_REFERENCE_U8)
-    assert kern == "k7_lds_n3"
+    assert kern == kname
     assert (got == orc.k1n_decode(K, g, rx, L)).all()
     ref, kern = genk_device_kernel(K, g, rx, L, native.VTB_GENK_K1_REFERENCE_U8, monkeypatch, force_genk=True)
     assert kern == "genk" and (ref == got).all()
     exact, kern = genk_device_kernel(K, g, rx, L, 0)
     ends = all((x >> (K - 1)) & 1 and x & 1 for x in g)
-    assert kern == ("k7_lds_n3" if ends else "genk"), (g, kern)
+    assert kern == (kname if ends else "genk"), (g, kern)
     assert (exact == orc.genk_decode(1, K, g, rx, L)).all()
 
 
-def test_k7n3_full_batch_and_persistent_grid(orc):
+@pytest.mark.parametrize("K", [7, 9])
+def test_n3_full_batch_and_persistent_grid(orc, K):
     """4,096 x 1,024 frames, 1,001 (one launch round) and a batch past what the CUs hold at once
     (the persistent loop) against the oracle, every frame; an odd frame count and a strided input."""
-    K, g = K7N3
+    g, kname = N3[K]
     L = 1024
     unc, rx = k1n_frames(orc, K, g, L, 4096, 0.06, 31)
     got, kern = genk_device_kernel(K, g, rx, L, native.VTB_GENK_K1_REFERENCE_U8)
-    assert kern in ("k7_lds_n3", "k7_lds_n3_loop")  # (7 waves per CU at 23.3 KB: 4,096 frames are 1.14 rounds)
+    assert kern in (kname, kname + "_loop")
     assert (got == orc.k1n_decode(K, g, rx, L)).all()
     got, kern = genk_device_kernel(K, g, rx[:1001], L, native.VTB_GENK_K1_REFERENCE_U8)
-    assert kern == "k7_lds_n3"
+    assert kern == kname
     assert (got == orc.k1n_decode(K, g, rx[:1001], L)).all()
-    big_unc, big = k1n_frames(orc, K, g, L, 2 * 7 * 256 * 2 + 3, 0.05, 32)
+    big_unc, big = k1n_frames(orc, K, g, L, 2 * 8 * 256 * 2 + 3, 0.05, 32)
     got, kern = genk_device_kernel(K, g, big, L, native.VTB_GENK_K1_REFERENCE_U8)
-    assert kern == "k7_lds_n3_loop"
+    assert kern == kname + "_loop" or (K == 9 and kern == kname)  # (K = 9: the CUs may hold the batch)
     assert (got == orc.k1n_decode(K, g, big, L)).all()
     # strided rows: the frames inside a wider buffer
     wide = np.zeros((65, big.shape[1] + 40), np.uint8)
@@ -182,14 +187,15 @@ def test_k7n3_full_batch_and_persistent_grid(orc):
     assert (out.cpu().numpy()[:, :L // 8] == orc.k1n_decode(K, g, big[:65], L)).all()
 
 
-def test_k7n3_reference_golden_on_fast_kernel():
-    """The reference's own k7n3 golden frames (tests/golden/k1n.npz) through the batch entry."""
+@pytest.mark.parametrize("name", ["k7n3", "k9n3"])
+def test_n3_reference_golden_on_fast_kernel(name):
+    """The reference's own golden frames (tests/golden/k1n.npz) through the batch entry."""
     z = load_golden("k1n.npz")
-    K, g = K7N3
-    keys = sorted({k.rsplit("_", 1)[0] for k in z if k.startswith("k7n3_L")})
+    K, g = K1N_PARAMS[name]
+    keys = sorted({k.rsplit("_", 1)[0] for k in z if k.startswith(name + "_L")})
     assert keys
     for key in keys:
         L = int(key.split("_")[1][1:])
         got, kern = genk_device_kernel(K, g, z[key + "_rx"], L, native.VTB_GENK_K1_REFERENCE_U8)
-        assert kern == "k7_lds_n3"
+        assert kern == N3[K][1]
         assert (got == z[key + "_decoded"]).all(), key
