@@ -1405,7 +1405,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         }
         return tb48(cb, l4);
     };
-    uint32_t loc = 0, loc_top = 0;  // survivor location as 4 l'
+    // survivor location as 4 l'.  Walks that start from an unknown location start at
+    // lane-dependent ones (any start is exact: the walk is verified), so that the first reads of
+    // up to 44 blocks do not all hit one LDS bank (round 3: soft -0.3 % per 4,096-frame launch,
+    // profiles/r03/ab_tbspread.txt)
+    uint32_t loc = known ? 0u : 4u * ((uint32_t(lane) * 37u) & 63u), loc_top = 0;
     for (int g = 0; g < nbody; g++) {
         const int tlo = start_full - 48 * (g + 1);
         if (g == kTbWarm / 48) loc_top = loc;
