@@ -1319,10 +1319,15 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         return;
     }
     const size_t units = SPLIT ? frames : (frames + 1) / 2;  // (persistent loop: pairs, or split frames)
-    if (LOOP && !GS && next < units) {
-        if constexpr (SPLIT) load_raw0_split<SOFT>(in, in_stride, T, t1s, warm, next, pra, prb);
-        else load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
-    }
+    // the next unit's chunk-0 input, waited for after this unit's traceback (split pass: after
+    // the fix-up, whose own loads and waits would otherwise queue behind it)
+    auto prefetch_next = [&]() {
+        if (LOOP && !GS && next < units) {
+            if constexpr (SPLIT) load_raw0_split<SOFT>(in, in_stride, T, t1s, warm, next, pra, prb);
+            else load_raw0<SOFT>(in, in_stride, frames, T, next, pra, prb);
+        }
+    };
+    if (!(SPLIT && sp)) prefetch_next();
     if (SPLIT && sp) {
         // frame A's metrics at t1 against frame B's at its step 96 (= t1), histories masked:
         // equal up to a constant -> B's decisions from t1 on are the frame's
@@ -1330,7 +1335,12 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         const uint32_t a = M & KEEP, b = (msave >> 16) & KEEP;
         const uint32_t a0 = __builtin_amdgcn_readfirstlane(a), b0 = __builtin_amdgcn_readfirstlane(b);
         bool conv = __ballot(((a - a0) & 0xFFFFu) == ((b - b0) & 0xFFFFu)) == ~0ull;
-        if (!conv && !SEG && !(dbg & 16384)) {  // VTB_DEBUG bit 14: no fix-up (measurement)
+        // VTB_DEBUG bit 15 (testing): the fix-up runs on every split frame, converged or not;
+        // bit 16 (testing): its checks never match, so every fix-up runs kFix chunks and the
+        // frame then takes the slow path.  Output must stay exact under both.
+        const bool fix_all = (dbg & 32768) != 0, fix_never = (dbg & 65536) != 0;
+        if ((!conv || fix_all) && !SEG && !(dbg & 16384)) {  // VTB_DEBUG bit 14: no fix-up (measurement)
+            conv = false;
             // Fix-up: frame B's half re-runs its steps from t1 on, now from frame A's metrics
             // at t1 (the frame's true metrics there), writing its survivor words over B's, one
             // chunk at a time until its metric vector equals B's own at the same step up to a
@@ -1350,14 +1360,18 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 const int t0 = warm + kChunk * j;
                 if (t0 + kChunk > t1s) break;  // past frame B's run: nothing left to compare
                 run_chunk(t0, std::true_type{}, std::false_type{});
-                const uint32_t fm = (M >> 16) & KEEP, bm = (ck[j] >> 16) & KEEP;
+                uint32_t ckj = ck[0];  // (ck[j] by selects: a dynamic index would put ck in scratch)
+#pragma unroll
+                for (int k = 1; k < kFix; k++) ckj = j == k ? ck[k] : ckj;
+                const uint32_t fm = (M >> 16) & KEEP, bm = (ckj >> 16) & KEEP;
                 const uint32_t f0 = __builtin_amdgcn_readfirstlane(fm), bm0 = __builtin_amdgcn_readfirstlane(bm);
-                conv = __ballot(((fm - f0) & 0xFFFFu) == ((bm - bm0) & 0xFFFFu)) == ~0ull;
+                conv = __ballot(((fm - f0) & 0xFFFFu) == ((bm - bm0) & 0xFFFFu)) == ~0ull && !fix_never;
             }
             fixp = false;
             baseA = baseA0;  // (the slow path below decodes frame A's rows again)
             __syncthreads();  // the rewritten words before the traceback reads them
         }
+        prefetch_next();
         if (!conv) {
             if constexpr (LOOP) {
                 // persistent split kernel: the list kernel decodes this frame afterwards
@@ -1423,9 +1437,17 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // (the last blocks are known).  Failed blocks whose successor is proven re-walk from it;
     // a re-walk can change their exit, so the checks repeat until every block is proven --
     // one round when all blocks merged within the warm-up.
+    // Rounds: every round proves at least the last unproven block of each chain (its successor
+    // is proven), so a chain of n blocks needs at most n rounds plus the one that sees no
+    // failure.  Unsplit frames are chains of at most 32 blocks; the split pass chains frame A's
+    // nA <= 32 blocks and frame B's blocks 2..31 into one chain of up to 62.  (Round 3 capped
+    // this loop at 33 rounds for both: a pure-noise split frame kept by the in-wave fix-up left
+    // frame A's first blocks unverified -- fuzz case 1366, 6 wrong bits at 85-93, DESIGN.md
+    // 4.2b.)  With 65 rounds no block can leave the loop unproven.
     uint32_t fin = loc;  // survivor's location at step blk * tbb
     bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement only): skip verification
-    for (int round = 0; round < 33; round++) {
+    const int rounds = (SPLIT && sp) ? 65 : 33;
+    for (int round = 0; round < rounds; round++) {
         // successor's exit (lane 31, frame A's last block, is known)
         const uint32_t sf = (SPLIT && sp) ? __shfl(fin, lane == nA - 1 ? kB0 : (lane + 1) & 63) : __shfl_down(fin, 1);
         const bool ok = fixed || loc_top == sf;

@@ -92,6 +92,12 @@ def main():
     run("single-frame, SEG off, no split", {"VTB_DEBUG": str(1024 | 256)}, "frame")
     run("batch decode_device", {}, "device")
     run("batch decode_device, no split", {"VTB_DEBUG": "256"}, "device")
+    # round 4 bisection: the in-wave fix-up off (bit 14), forced on every split frame (bit 15),
+    # forced and never converging (bits 15 + 16)
+    run("single-frame, SEG off, no fix-up", {"VTB_DEBUG": str(1024 | 16384)}, "frame")
+    run("batch decode_device, no fix-up", {"VTB_DEBUG": "16384"}, "device")
+    run("batch decode_device, fix-up on every frame", {"VTB_DEBUG": "32768"}, "device")
+    run("batch decode_device, fix-up never converging", {"VTB_DEBUG": str(32768 | 65536)}, "device")
 
 
 if __name__ == "__main__":
