@@ -972,9 +972,17 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
                  "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
+#ifdef VTB_EXP_STAGE48
+        // measurement: lanes 48-63 (duplicates of rows 0-15) skip the staging writes, so the
+        // second 32-lane group of each write has no two lanes on one bank (round 4 LDS-conflict A/B)
+        if (lane < kChunk) {
+#endif
         VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+#ifdef VTB_EXP_STAGE48
+        }
+#endif
 #undef VTB_W2
         if (SEG) {
             // either half may hold padding rows (steps >= Ta in A, >= Tb in B): own-keeping rows

@@ -114,6 +114,12 @@ __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b
 // (sc1), the words another workgroup reads in the same launch (k9_seg_kernel).
 template <int OFF, bool SC = false>
 __device__ __forceinline__ void gstore(uint32_t vo, uint32_t z, uint64_t base) {
+#ifdef VTB_EXP_K9_NOWORD
+    // measurement only (wrong results): the survivor words are formed but never stored, to bound
+    // what keeping them on the CU could save; run with VTB_DEBUG=1 (no traceback)
+    asm volatile("" ::"v"(vo), "v"(z), "s"(base));
+    return;
+#endif
     if constexpr (SC)
         asm volatile("global_store_dword %0, %1, %2 offset:%3 sc1" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
     else
@@ -653,7 +659,11 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             if constexpr (I == 20) {
                 // one survivor store batch (step 15) was issued after the loads (SEG: LDS loads)
                 if constexpr (SEG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
+#ifdef VTB_EXP_K9_NOWORD
+                else asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
+#else
                 else asm volatile("s_waitcnt vmcnt(4)" : "+v"(ra), "+v"(rb));
+#endif
                 stage_compute(ra, rb, se, set);
             }
             if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);  // all rows of this chunk read

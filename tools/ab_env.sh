@@ -15,7 +15,7 @@ for r in $(seq $reps); do
   for a in "${arms[@]}"; do
     label=${a%%=*}; vars=${a#*=}
     env $vars timeout -k 10 120 python3 bench.py --steps 100 --warmup 10 --cpu-seconds 0 "$@" > gpurun_out/ab_env_$label.log 2>&1 || exit $?
-    echo "$label $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/ab_env_$label.log | cut -d' ' -f2) $(grep -o '"value": [0-9.]*' gpurun_out/ab_env_$label.log | cut -d' ' -f2)" >> $out
+    echo "$label $(grep -o '"kernel_avg_ms": [0-9.]*' gpurun_out/ab_env_$label.log | cut -d' ' -f2) $(grep -o '"value": [0-9.]*' gpurun_out/ab_env_$label.log | cut -d' ' -f2)" >> $out
   done
 done
 sort $out

@@ -17,7 +17,7 @@ for r in $(seq $reps); do
   for d in convolutionalencdec_amd/lib/exp/*/; do
     n=$(basename $d)
     VTB_LIB_PATH=$PWD/$d/libviterbi_amd.so timeout -k 10 120 python3 bench.py --steps 100 --warmup 10 --cpu-seconds 0 "$@" > $o/ab_$n.log 2> $o/ab_$n.err || exit $?
-    echo "$n $(grep -o '"kernel_ms": [0-9.]*' $o/ab_$n.log | cut -d' ' -f2) $(grep -o '"value": [0-9.]*' $o/ab_$n.log | cut -d' ' -f2)" >> $o/ab.txt
+    echo "$n $(grep -o '"kernel_avg_ms": [0-9.]*' $o/ab_$n.log | cut -d' ' -f2) $(grep -o '"value": [0-9.]*' $o/ab_$n.log | cut -d' ' -f2)" >> $o/ab.txt
   done
 done
 sort $o/ab.txt

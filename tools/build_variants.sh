@@ -42,6 +42,8 @@ for v in "$@"; do
     sgmask) build sgmask -DVTB_EXP_SGMASK ;;
     e32sg) build e32sg -DVTB_EXP_E32 -DVTB_EXP_SGMASK ;;
     b128) build b128 -DVTB_EXP_B128 ;;
+    k9noword) build k9noword -DVTB_EXP_K9_NOWORD ;;
+    stage48) build stage48 -DVTB_EXP_STAGE48 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

@@ -17,7 +17,7 @@ for r in $(seq $reps); do
     python3 - "$n" "$steps" gpurun_out/inflight_$n.json >> $out <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
-print(sys.argv[1], sys.argv[2], d["ms_per_step"], d["value"], d["roofline"]["kernel_ms"])
+print(sys.argv[1], sys.argv[2], d["ms_per_step"], d["value"], d["roofline"]["kernel_avg_ms"])
 EOF
   done
 done

@@ -18,7 +18,7 @@ DECODERS = ("k7_lds_kernel", "k9_kernel", "lds_path")
 
 def main():
     root, key = sys.argv[1], sys.argv[2]
-    paths = glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True)
+    paths = glob.glob(os.path.join(root, "**", "*kernel_stats*.csv"), recursive=True)
     if not paths:
         raise SystemExit(f"no kernel_stats.csv under {root}")
     best = None
