@@ -122,8 +122,13 @@ __device__ __forceinline__ void gstore(uint32_t vo, uint32_t z, uint64_t base) {
 #endif
     if constexpr (SC)
         asm volatile("global_store_dword %0, %1, %2 offset:%3 sc1" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+#ifdef VTB_EXP_K9_NT
+    else  // measurement: survivor words stored non-temporal (streaming L2 policy)
+        asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+#else
     else
         asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
+#endif
 }
 
 // Words handed from one workgroup to another inside a launch: global (never flat) agent-scope

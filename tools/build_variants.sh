@@ -44,6 +44,7 @@ for v in "$@"; do
     b128) build b128 -DVTB_EXP_B128 ;;
     k9noword) build k9noword -DVTB_EXP_K9_NOWORD ;;
     stage48) build stage48 -DVTB_EXP_STAGE48 ;;
+    k9nt) build k9nt -DVTB_EXP_K9_NT ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

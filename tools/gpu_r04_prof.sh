@@ -6,7 +6,4 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 bash tools/pmc_r04.sh ${WL:-head c2 c3s c3h c4 c5} || exit 1
-TAG=head bash tools/pmc_stalls.sh || exit 1
-TAG=notb VTB_DEBUG=1 bash tools/pmc_stalls.sh || exit 1
-TAG=c4 BARGS="--K 9 --hard" bash tools/pmc_stalls.sh || exit 1
 echo "prof passes done"
