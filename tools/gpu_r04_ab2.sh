@@ -10,4 +10,5 @@ VARIANTS="$E/base $E/k9nt" bash tools/ab_variants.sh 3 --K 9 --hard && cp gpurun
 TAG=head bash tools/pmc_stalls.sh || exit 1
 TAG=notb VTB_DEBUG=1 bash tools/pmc_stalls.sh || exit 1
 TAG=c4 BARGS="--K 9 --hard" bash tools/pmc_stalls.sh || exit 1
+bash tools/configs.sh && cp gpurun_out/configs.jsonl gpurun_out/r04/configs.jsonl || exit 1
 echo "ab2 done"
