@@ -160,6 +160,15 @@ __device__ __forceinline__ void candidates(uint32_t (&M)[4], const uint2 (&vw)[4
     } else if constexpr (P == 5 || P == 4) {
         // The adds separate the last VALU write of each M[r] from its swap; the s_nop the
         // last swap from the first read of a result (one wait state each way).
+#ifdef VTB_EXP_K9_NOSWAP
+        // measurement only (wrong results): plain moves instead of the swaps, to price them
+        asm volatile(
+            "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"
+            "v_mov_b32 %4, %4\n\tv_mov_b32 %5, %5\n\tv_mov_b32 %6, %6\n\tv_mov_b32 %7, %7"
+            : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3]), "+v"(M[0]), "+v"(M[1]), "+v"(M[2]), "+v"(M[3])
+            : "v"(vw[0].x), "v"(vw[1].x), "v"(vw[2].x), "v"(vw[3].x));
+        if constexpr (false)
+#endif
         if constexpr (P == 5) {
             asm volatile(
                 "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"

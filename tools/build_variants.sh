@@ -45,6 +45,7 @@ for v in "$@"; do
     k9noword) build k9noword -DVTB_EXP_K9_NOWORD ;;
     stage48) build stage48 -DVTB_EXP_STAGE48 ;;
     k9nt) build k9nt -DVTB_EXP_K9_NT ;;
+    k9noswap) build k9noswap -DVTB_EXP_K9_NOSWAP ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
