@@ -106,7 +106,10 @@ constexpr int ring_bytes(int NB) { return (2 << NB) * (NB == 3 ? kColN<3> : kCol
 constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
 // Share of its chunks the second-dispatched wave of a SIMD runs at priority 1 (wave balance,
 // k7_pair).  55 / 59 / 63 measured alike (31.06 / 31.1 / 31.0 us per 4,096-frame launch).
-constexpr int kPrioPct = 59;
+#ifndef VTB_EXP_PRIO
+#define VTB_EXP_PRIO 59
+#endif
+constexpr int kPrioPct = VTB_EXP_PRIO;
 constexpr uint32_t kR1 = 0x10001u;
 
 // History bits per u16 half: soft input keeps 4m + h (2 history bits, the

@@ -46,6 +46,7 @@ for v in "$@"; do
     stage48) build stage48 -DVTB_EXP_STAGE48 ;;
     k9nt) build k9nt -DVTB_EXP_K9_NT ;;
     k9noswap) build k9noswap -DVTB_EXP_K9_NOSWAP ;;
+    prio*) build $v -DVTB_EXP_PRIO=${v#prio} ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
