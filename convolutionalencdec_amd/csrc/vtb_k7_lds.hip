@@ -105,9 +105,11 @@ constexpr int ring_bytes(int NB) { return (2 << NB) * (NB == 3 ? kColN<3> : kCol
 #endif
 constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
 // Share of its chunks the second-dispatched wave of a SIMD runs at priority 1 (wave balance,
-// k7_pair).  55 / 59 / 63 measured alike (31.06 / 31.1 / 31.0 us per 4,096-frame launch).
+// k7_pair).  Round 2: 55 / 59 / 63 measured alike (31.06 / 31.1 / 31.0 us per 4,096-frame launch);
+// round 4, ten interleaved rounds over two boxes (profiles/r04/first/ab_prio_*.txt): 67 is
+// 0.4-0.6 % faster than 59, 50 / 71 / 75 slower.
 #ifndef VTB_EXP_PRIO
-#define VTB_EXP_PRIO 59
+#define VTB_EXP_PRIO 67
 #endif
 constexpr int kPrioPct = VTB_EXP_PRIO;
 constexpr uint32_t kR1 = 0x10001u;
