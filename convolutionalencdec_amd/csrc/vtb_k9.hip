@@ -662,8 +662,20 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     // T - 1 hold each location's own even decision (bit 0 of each half), kept in msave for the
     // survivor fix-up below (the ACS of step T may carry another location's bit 0 into l)
     const int tsave = (STREAM && SOFT && sa.last && (T & 1)) ? T - 1 : -1;
+#ifdef VTB_EXP_K9PRIO
+    // measurement: the K=7 kernel's wave balance (vtb_k7_lds.hip kPrioPct): the second-dispatched
+    // wave of a SIMD (HW_ID wave slot 1) at priority 1 for the first VTB_EXP_K9PRIO % of its chunks
+    uint32_t hwid9;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid9));
+    const bool second9 = !SEG && (hwid9 & 1u) != 0;
+    const int hi9 = VTB_EXP_K9PRIO * ((tacs - tbeg) / kCh) / 100;
+#endif
     for (int t0 = tbeg; t0 < tacs; t0 += kCh) {
         const int c0 = t0 / kCh;
+#ifdef VTB_EXP_K9PRIO
+        if (second9 && (t0 - tbeg) / kCh < hi9) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
         // survivor column of step t0 (streaming: position in the ring)
         const uint32_t gvo = uint32_t(kColBytes) * uint32_t((STREAM ? t0 % sa.ring : t0) >> 4) + wlane;
         static_for(std::make_integer_sequence<int, kCh>{}, [&](auto ic) {
@@ -750,6 +762,9 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                 for (int r = 0; r < 4; r++) msave[r] = M[r];
         }
     }
+#ifdef VTB_EXP_K9PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     if constexpr (SEG) {

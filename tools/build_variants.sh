@@ -47,6 +47,7 @@ for v in "$@"; do
     k9nt) build k9nt -DVTB_EXP_K9_NT ;;
     k9noswap) build k9noswap -DVTB_EXP_K9_NOSWAP ;;
     prio*) build $v -DVTB_EXP_PRIO=${v#prio} ;;
+    k9prio*) build $v -DVTB_EXP_K9PRIO=${v#k9prio} ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
