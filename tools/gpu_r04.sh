@@ -18,7 +18,7 @@ for s in "$@"; do
     seed1017) VTB_FUZZ_N=2000 VTB_FUZZ_SEED=1017 timeout -k 10 1100 python3 -u -m pytest tests/test_gpu_fuzz.py -q \
                -p no:cacheprovider --timeout 300 --timeout-method thread > $o/fuzz_seed1017.log 2>&1 \
                || { tail -40 $o/fuzz_seed1017.log; exit 1; } ; tail -3 $o/fuzz_seed1017.log ;;
-    fuzz:*) sd="${s#fuzz:}"; VTB_FUZZ_N=2000 VTB_FUZZ_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fuzz.py -q \
+    fuzz:*) sd="${s#fuzz:}"; VTB_FUZZ_N=${FUZZ_N:-2000} VTB_FUZZ_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fuzz.py -q \
                -p no:cacheprovider --timeout 300 --timeout-method thread > $o/fuzz_seed$sd.log 2>&1 \
                || { tail -40 $o/fuzz_seed$sd.log; exit 1; } ; tail -2 $o/fuzz_seed$sd.log ;;
     fixup:*) sd="${s#fixup:}"; VTB_FIXUP_N=2000 VTB_FIXUP_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_split_fixup.py -q \
