@@ -75,3 +75,50 @@ def test_soft_period_16_overflows_padding():
 
 def test_shipped_soft_period_is_12():
     assert shipped_period() == 12
+
+
+K9_SRC = os.path.join(os.path.dirname(SRC), "vtb_k9.hip")
+
+
+def worst_candidate_k9(soft, nb):
+    """The same worst case for the K=9 kernel (vtb_k9.hip): bias B = SC·8·n·Q (8 = K - 1), a
+    12-step soft period (steps 10 / 11) or one renormalisation per 48-step chunk (hard, steps
+    40 / 47); soft padding steps run on clamped input (their survivor bits are overwritten
+    after the ACS), hard padding rows add W = SC·(8·n·Q + 1)."""
+    q = 255 if soft else 1
+    sc = 4 if soft else 256
+    emax, spread = nb * q, 8 * nb * q
+    bias = spread
+    read, apply, between = (10, 11, 12) if soft else (40, 47, 48)
+    m_after = bias + spread + (apply - read + 1) * emax
+    m = max(m_after + (between - 1) * emax, bias + q + (apply + 1) * emax)  # start value (uint8)(257)·Q = Q
+    tie = sc // 2
+    own = sc * (m + emax) + (sc - 1) + tie
+    pad = 0 if soft else sc * m + (sc - 1) + sc * (spread + 1) + tie
+    return max(own, pad), m
+
+
+def test_k9_constants_match_model():
+    src = open(K9_SRC).read()
+    assert "constexpr uint32_t B4 = H::SC * 8 * NB * Q;" in src
+    assert "PADW = H::SC * ((SOFT ? 2 : 8 * NB) * Q + 1) * kR1;" in src
+    assert re.search(r"RN_READ = SOFT \? \(I % 12\) == 10 : I == 40;", src)
+    assert re.search(r"RN_APPLY = SOFT \? \(I % 12\) == 11 : I == 47;", src)
+
+
+@pytest.mark.parametrize("soft,nb", [(True, 2), (False, 2), (False, 3)],
+                         ids=["soft", "hard", "hard-rate1/3"])
+def test_k9_metrics_fit_u16(soft, nb):
+    worst, m = worst_candidate_k9(soft, nb)
+    assert worst < U16, (worst, m)
+    if not soft:
+        assert m < 256
+
+
+def test_k7_constants_match_model():
+    src = open(SRC).read()
+    assert "constexpr uint32_t INIT = 6 * NB * Q + 1;" in src
+    assert "static constexpr uint32_t BIAS = SC * (SOFT ? 3060 : 6 * NB);" in src
+    assert "constexpr uint32_t PADW = H::SC * INIT * kR1;" in src
+    assert "#define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)" in src
+    assert "#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)" in src
