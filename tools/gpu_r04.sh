@@ -21,7 +21,7 @@ for s in "$@"; do
     fuzz:*) sd="${s#fuzz:}"; VTB_FUZZ_N=${FUZZ_N:-2000} VTB_FUZZ_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fuzz.py -q \
                -p no:cacheprovider --timeout 300 --timeout-method thread > $o/fuzz_seed$sd.log 2>&1 \
                || { tail -40 $o/fuzz_seed$sd.log; exit 1; } ; tail -2 $o/fuzz_seed$sd.log ;;
-    fixup:*) sd="${s#fixup:}"; VTB_FIXUP_N=2000 VTB_FIXUP_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_split_fixup.py -q \
+    fixup:*) sd="${s#fixup:}"; VTB_FIXUP_N=${FIXUP_N:-2000} VTB_FIXUP_SEED=$sd timeout -k 10 600 python3 -u -m pytest tests/test_gpu_split_fixup.py -q \
                -p no:cacheprovider --timeout 300 --timeout-method thread -k fixup_family > $o/fixup_seed$sd.log 2>&1 \
                || { tail -40 $o/fixup_seed$sd.log; exit 1; } ; tail -2 $o/fixup_seed$sd.log ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { cat $o/smoke.log; exit 1; } ;;
