@@ -30,6 +30,7 @@ struct vtb_plan {
     int32_t T;
     int device;
     uint8_t symm[1 << (vtb::kMaxS - 1)];
+    vtb::Knobs knobs;  // read from the environment once, at creation (vtb_internal.h)
     // host-path staging (grown on demand)
     uint8_t* d_in = nullptr;
     uint8_t* d_out = nullptr;
@@ -75,6 +76,7 @@ struct vtb_stream {
     int t_begin = 0;              // steps decoded in the current frame (multiple of 48)
     int carry_len = 0;            // segments received but not yet decoded (< 48)
     bool gen = false;             // generic kernel (vtb_stream_gen.hip): K other than 7, 9; no carry
+    vtb::Knobs knobs;             // read once, at creation
 };
 
 namespace {
@@ -119,16 +121,11 @@ size_t in_bytes(const vtb_code_t* c, vtb_input_t in, int32_t L) {
 
 size_t out_bytes(int32_t L) { return (size_t(L) + 7) / 8; }
 
-bool env_flag_is(const char* name, const char* value) {
-    const char* v = std::getenv(name);
-    return v && std::strcmp(v, value) == 0;
-}
-
 // Which kernel family a plan uses (see below).  VTB_KERNEL=k7|gws|k9|lds forces one (testing
-// and A/B measurement); a forced kernel that does not support the shape is an error.
-// (VTB_KERNEL=seg leaves the choice here free and only forbids nothing: the single-frame
-// path's SEG kernel is chosen in vtb_decode_frame_sync, and any other forced family turns it
-// off there.)
+// and A/B measurement, read into the plan's knobs at creation); a forced kernel that does not
+// support the shape is an error.  (VTB_KERNEL=seg leaves the choice here free: the single-frame
+// path's SEG kernel is chosen in vtb_decode_frame_sync, and any other forced family turns it off
+// there.)
 int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, size_t out_stride,
            size_t frames, hipStream_t stream) {
     vtb::Launch a;
@@ -144,14 +141,19 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     a.stream = stream;
     a.cus = p->cus;
     a.tstamp = vtb::debug_tstamp();
+    a.guard_hits = vtb::debug_guard_hits();
+    a.dbg = p->knobs.dbg;
+    a.split_warm_force = p->knobs.split_warm;
+    a.seg9_xcd = p->knobs.seg9_xcd;
     std::memcpy(a.symm, p->symm, sizeof(a.symm));
-    const char* force = std::getenv("VTB_KERNEL");
-    const bool k7s = env_flag_is("VTB_KERNEL", "k7s");  // prefer the persistent split kernel (below)
-    const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg") || k7s;  // (seg: vtb_decode_frame_sync)
-    const bool want_k7 = any || env_flag_is("VTB_KERNEL", "k7");
-    const bool want_gws = any || env_flag_is("VTB_KERNEL", "gws");
-    const bool want_lds = any || env_flag_is("VTB_KERNEL", "lds");
-    const bool want_k9 = any || env_flag_is("VTB_KERNEL", "k9");
+    using vtb::Force;
+    const Force force = p->knobs.force;
+    const bool k7s = force == Force::K7s;  // prefer the persistent split kernel (below)
+    const bool any = force == Force::Any || force == Force::Seg || k7s;  // (seg: vtb_decode_frame_sync)
+    const bool want_k7 = any || force == Force::K7;
+    const bool want_gws = any || force == Force::Gws;
+    const bool want_lds = any || force == Force::Lds;
+    const bool want_k9 = any || force == Force::K9;
     hipError_t e;
     // K=7: survivors in LDS while that LDS leaves the CU as many waves (2 frames each) as
     // the batch can give it, up to 2 per SIMD (the ACS is VALU-bound there: more waves do
@@ -191,7 +193,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     // (7.5x the algorithmic HBM bytes).  VTB_KERNEL=k7s forces it wherever it applies;
     // VTB_DEBUG bit 12 (measurement only): never.
     const bool want_split = k7s || (any && !k7_in_lds);
-    if (want_split && !(vtb::debug_flags() & 4096) && vtb::k7_split_loop_supported(a)) {
+    if (want_split && !(a.dbg & 4096) && vtb::k7_split_loop_supported(a)) {
         if (!workspace(vtb::k7_split_loop_workspace_bytes(a))) return VTB_ERR_NOMEM;
         e = vtb::launch_k7_split_loop(a);
         if (e == hipErrorOutOfMemory) return VTB_ERR_NOMEM;
@@ -359,6 +361,40 @@ const char* last_kernel() { return t_last_kernel; }
 unsigned long long* debug_tstamp() { return g_tstamp; }
 void set_debug_tstamp(unsigned long long* p) { g_tstamp = p; }
 
+namespace {
+std::atomic<uint32_t*> g_guard_hits{nullptr};
+}  // namespace
+uint32_t* debug_guard_hits() { return g_guard_hits.load(std::memory_order_relaxed); }
+void set_debug_guard_hits(uint32_t* p) { g_guard_hits.store(p, std::memory_order_relaxed); }
+
+Knobs read_knobs() {
+    auto num = [](const char* name, int dflt) {
+        const char* v = std::getenv(name);
+        return v && *v ? std::atoi(v) : dflt;
+    };
+    Knobs k;
+    k.dbg = num("VTB_DEBUG", 0) & kDbgHonoured;
+    if (const char* v = std::getenv("VTB_KERNEL"); v && *v) {
+        static const struct {
+            const char* name;
+            Force f;
+        } names[] = {{"k7", Force::K7}, {"gws", Force::Gws}, {"k9", Force::K9}, {"lds", Force::Lds},
+                     {"seg", Force::Seg}, {"k7s", Force::K7s}, {"genk", Force::Genk}};
+        k.force = Force::Unknown;  // (an unknown name forces no family that exists: unsupported)
+        for (const auto& n : names)
+            if (std::strcmp(v, n.name) == 0) k.force = n.f;
+    }
+    k.split_warm = num("VTB_SPLIT_WARM", 0);
+    k.genk_warm = num("VTB_GENK_WARM", -1);
+    k.seg_waves = num("VTB_SEG_WAVES", 0);
+    k.seg_warm = num("VTB_SEG_WARM", 0);
+    k.seg_adapt = num("VTB_SEG_ADAPT", 1) != 0;
+    k.seg9_wgs = num("VTB_SEG9_WGS", 0);
+    k.seg9_waves = num("VTB_SEG9_WAVES", 0);
+    k.seg9_xcd = num("VTB_SEG9_XCD", -1);
+    return k;
+}
+
 }  // namespace vtb
 
 extern "C" {
@@ -374,6 +410,17 @@ const char* vtb_debug_last_kernel(void) { return vtb::last_kernel(); }
 // Measurement only (not in include/viterbi_amd.h): device buffer of 8 u64 per wave that the
 // next K=7 frame launches fill with phase timestamps (tools/tstamp.py); nullptr turns it off.
 void vtb_debug_set_tstamp(unsigned long long* d_buf) { vtb::set_debug_tstamp(d_buf); }
+
+// Testing only (not in include/viterbi_amd.h): a device word (uint32) to which every traceback
+// completeness guard that fires in later launches adds 1 -- a verified block-parallel chain left
+// unproven after its round cap, its frame sent to the exact slow path (vtb_internal.h
+// kDbgTbCap); nullptr turns it off.
+void vtb_debug_set_guard_counter(uint32_t* d_word) { vtb::set_debug_guard_hits(d_word); }
+
+// Testing only: the VTB_DEBUG bits a plan created now would carry.  The shipped library drops
+// the output-corrupting bits 0-4 (vtb_internal.h kDbgUnsafe); a -DVTB_MEASURE build keeps them.
+int vtb_debug_effective_flags(void) { return vtb::read_knobs().dbg; }
+int vtb_debug_measure_build(void) { return vtb::kDbgHonoured == ~0 ? 1 : 0; }
 
 // Measurement only (not in include/viterbi_amd.h): frames of the plan's last persistent split
 // launch that did not converge split (re-decoded by the list kernel); synchronises the device.
@@ -451,6 +498,7 @@ int vtb_plan_create(vtb_plan_t** plan, const vtb_code_t* code, vtb_input_t input
     p->L = frame_bits;
     p->T = frame_bits + code->constraint_length - 1;
     p->device = device;
+    p->knobs = vtb::read_knobs();
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
@@ -824,7 +872,8 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     // K = 7 and K = 9: their own kernels (survivor words packed per 48-step chunk, a carry of
     // < 48 segments between calls); every other K (and K = 7 / 9 with VTB_KERNEL=lds, for
     // testing): the generic stream kernel, all segments of a call at once
-    const bool gen = (K != 7 && K != 9) || env_flag_is("VTB_KERNEL", "lds");
+    const vtb::Knobs knobs = vtb::read_knobs();
+    const bool gen = (K != 7 && K != 9) || knobs.force == vtb::Force::Lds;
     const bool k9 = K == 9 && !gen;
     if (input != VTB_INPUT_HARD && input != VTB_INPUT_SOFT8) return VTB_ERR_INVALID;
     if (streams == 0 || streams > (size_t(1) << 31)) return VTB_ERR_INVALID;
@@ -846,6 +895,7 @@ int vtb_stream_create(vtb_stream_t** sp, const vtb_code_t* code, vtb_input_t inp
     s->ring = int(win);
     s->device = device;
     s->gen = gen;
+    s->knobs = knobs;
     edge_table(code, s->symm);
     if (gen) {
         const int S = K - 1;
@@ -924,6 +974,8 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
         a.frames = s->streams;
         a.stream = hs;
         a.ws = s->d_ring;
+        a.dbg = s->knobs.dbg;
+        a.guard_hits = vtb::debug_guard_hits();
         std::memcpy(a.symm, s->symm, sizeof(a.symm));
         vtb::StreamArgs sa;
         sa.state = s->d_state;
@@ -961,6 +1013,8 @@ int vtb_stream_decode(vtb_stream_t* s, const uint8_t* d_in, size_t in_stride, in
         a.frames = s->streams;
         a.stream = hs;
         a.ws = s->d_ring;
+        a.dbg = s->knobs.dbg;
+        a.guard_hits = vtb::debug_guard_hits();
         std::memcpy(a.symm, s->symm, sizeof(a.symm));
         vtb::StreamArgs sa;
         sa.state = s->d_state;
@@ -1031,33 +1085,28 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
             return VTB_ERR_NOMEM;
         }
         std::memset(plan->lat_in, 0, (ib + 32) / 16 * 16);
-        // SEG kernel geometry, read once per plan ($VTB_SEG_WAVES / $VTB_SEG_WARM: measurement)
-        // eight waves (two per SIMD, 16 segments: 128.5 against 120 Mbit/s for four in the
-        // reference's speedDecode); four where eight waves' survivor words do not
-        // fit the CU's LDS (frames past about 12,000 bits)
-        int waves = 8, warm = vtb::kSegWarm;
-        const char* wenv = std::getenv("VTB_SEG_WAVES");
-        if (wenv) waves = std::atoi(wenv);
-        if (const char* v = std::getenv("VTB_SEG_WARM")) warm = std::atoi(v);
+        // SEG kernel geometry, once per plan ($VTB_SEG_WAVES / $VTB_SEG_WARM in the plan's knobs:
+        // measurement): eight waves (two per SIMD, 16 segments: 128.5 against 120 Mbit/s for four
+        // in the reference's speedDecode); four where eight waves' survivor words
+        // do not fit the CU's LDS (frames past about 12,000 bits)
+        const vtb::Knobs& kn = plan->knobs;
+        int waves = kn.seg_waves > 0 ? kn.seg_waves : 8, warm = kn.seg_warm > 0 ? kn.seg_warm : vtb::kSegWarm;
         vtb::Launch a;
         a.S = plan->code.constraint_length - 1;
         a.soft = plan->input == VTB_INPUT_SOFT8;
         a.T = plan->T;
         a.L = plan->L;
-        const char* force = std::getenv("VTB_KERNEL");
-        const bool any = !force || !*force || env_flag_is("VTB_KERNEL", "seg");
-        if (!wenv && !vtb::k7_seg_supported(a, waves, warm)) waves = 4;
-        plan->seg_waves = any && !(vtb::debug_flags() & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
+        const bool any = kn.force == vtb::Force::Any || kn.force == vtb::Force::Seg;
+        if (kn.seg_waves <= 0 && !vtb::k7_seg_supported(a, waves, warm)) waves = 4;
+        plan->seg_waves = any && !(kn.dbg & 1024) && vtb::k7_seg_supported(a, waves, warm) ? waves : 0;
         plan->seg_warm = warm;
-        const char* adapt = std::getenv("VTB_SEG_ADAPT");  // "0": the plan's warm-up only (measurement)
-        const bool short_ok = !std::getenv("VTB_SEG_WARM") && !(adapt && std::atoi(adapt) == 0);
+        // $VTB_SEG_ADAPT=0: the plan's warm-up only (measurement)
+        const bool short_ok = kn.seg_warm <= 0 && kn.seg_adapt;
         plan->seg_short = short_ok && plan->seg_waves > 0 && vtb::k7_seg_supported(a, waves, vtb::kSegWarmShort);
         plan->seg_backoff = kSegBackoff0;
-        // K = 9: the frame over several workgroups ($VTB_SEG9_WGS: measurement)
-        int wgs = vtb::kSeg9Wgs, w9 = vtb::kSeg9Waves;
-        if (const char* v = std::getenv("VTB_SEG9_WGS")) wgs = std::atoi(v);
-        if (const char* v = std::getenv("VTB_SEG9_WAVES")) w9 = std::atoi(v);
-        if (any && !(vtb::debug_flags() & 1024) && vtb::k9_seg_supported(a, w9, wgs, vtb::kSeg9Warm)) {
+        // K = 9: the frame over several workgroups ($VTB_SEG9_WGS / _WAVES: measurement)
+        const int wgs = kn.seg9_wgs > 0 ? kn.seg9_wgs : vtb::kSeg9Wgs, w9 = kn.seg9_waves > 0 ? kn.seg9_waves : vtb::kSeg9Waves;
+        if (any && !(kn.dbg & 1024) && vtb::k9_seg_supported(a, w9, wgs, vtb::kSeg9Warm)) {
             const bool s9 = short_ok && vtb::k9_seg_supported(a, w9, wgs, vtb::kSegWarmShort);
             const size_t wsb = std::max(vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSeg9Warm),
                                         s9 ? vtb::k9_seg_workspace_bytes(a, w9, wgs, vtb::kSegWarmShort) : size_t(0));
@@ -1102,6 +1151,9 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         a.frames = 1;
         a.stream = plan->stream;
         a.cus = plan->cus;
+        a.dbg = plan->knobs.dbg;
+        a.seg9_xcd = plan->knobs.seg9_xcd;
+        a.guard_hits = vtb::debug_guard_hits();
         std::memcpy(a.symm, plan->symm, sizeof(a.symm));
         if (plan->seg_waves > 0) {
             if (vtb::launch_k7_seg(a, plan->seg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;

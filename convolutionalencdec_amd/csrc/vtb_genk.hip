@@ -40,6 +40,7 @@ struct GenArgs {
     int u8;          // VTB_GENK_K1_REFERENCE_U8: the reference's k=1 butterfly arithmetic (below)
     int warm;        // traceback warm-up steps per block (any value is exact: the walk is verified)
     int dbg;         // $VTB_DEBUG (measurement only): bit 0 skips the traceback, bit 1 the ACS
+    uint32_t* hits;  // testing: completeness-guard counter (Launch::guard_hits), null in production
     uint32_t rg[8];  // generators bit-reversed over k*K bits (convEncode.c:163-174)
 };
 
@@ -374,19 +375,34 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         for (int i = start - 1; active && i >= top; i--) s = ptr(i, s);
         int s_top = s;
         for (int i = top - 1; active && i >= lo; i--) s = ptr(i, s);
+        // (one chain of up to 64 blocks: at most 63 re-walk rounds.)  Completeness guard: a block
+        // still unproven after the cap (VTB_DEBUG bit 17: one round) sends the frame to its
+        // serial walk -- lane 0 emits every window from state 0 at the last boundary
         int fin = s;
         bool fixed = !active || start == nb;
-        for (int round = 0; round < 65; round++) {
+        const int rounds = (a.dbg & kDbgTbCap) ? 1 : 65;
+        bool unproven = false;
+        for (int round = 0;; round++) {
             const int sf = __shfl_down(fin, 1);
             const bool ok = fixed || s_top == sf;
             const uint64_t bad = ~__ballot(ok);
             if (bad == 0) break;
+            if (round == rounds) {
+                unproven = true;
+                break;
+            }
             if (!ok && (bad >> (lane + 1)) == 0) {
                 s_top = s = sf;
                 for (int i = top - 1; i >= lo; i--) s = ptr(i, s);
                 fin = s;
                 fixed = true;
             }
+        }
+        int elo = lo, etop = top;  // emitted boundaries [elo, etop), from s_top at etop - 1
+        bool emit = active;
+        if (unproven) {
+            emit = lane == 0, elo = 0, etop = nb, s_top = 0;
+            if (lane == 0) note_guard(a.hits);
         }
         // window i holds the inputs of steps t_b + (i-1) S + 1 .. t_b + i S: the kS bits of the
         // state at boundary i, oldest (its top bits) first, at stream bit p0 = (t_b + (i-1) S + 1) k
@@ -404,7 +420,7 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
             acc |= v << (8 * (byte & 3));
         };
         s = s_top;
-        for (int i = top - 1; active && i >= lo; i--) {
+        for (int i = etop - 1; emit && i >= elo; i--) {
             if (i < nb - 1) {
                 int p0 = (tb0 + (i - 1) * S + 1) * k, w = kS;
                 uint32_t fv = uint32_t(s);
@@ -450,19 +466,22 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     if (in_stride < size_t(T) || out_stride < size_t((info_bits + 7) / 8)) return VTB_ERR_INVALID;
     if (frames == 0) return VTB_OK;
     hipStream_t st = (hipStream_t)stream;
+    // testing knobs (vtb_internal.h), read per call: this entry point has no plan to hold them
+    const vtb::Knobs kn = vtb::read_knobs();
     // k = 1, K = 7 or 9, rate 1/3, hard segments: the K=7 LDS pair kernel / the K=9 frame kernel
     // with a 16-column table (vtb_k7_lds.hip k7_pair NB = 3, vtb_k9.hip k9_pair NB = 3).  Its butterfly takes the upper predecessor's branch
     // metric as n - e (reference viterbiDecoderButterflyk1.c:104-107): the reference's own
     // arithmetic for any generators, and the exact one when every generator taps both ends.
     // Its exact metrics equal the reference's uint8 ones at n = 3 (the minimum grows by at most
     // one per step, so nothing wraps: DESIGN.md §3, §4.7).  VTB_KERNEL=genk keeps this kernel.
-    if (k == 1 && (K == 7 || K == 9) && n == 3 && !vtb::env_is("VTB_KERNEL", "genk")) {
+    if (k == 1 && (K == 7 || K == 9) && n == 3 && kn.force != vtb::Force::Genk) {
         bool ends = true;
         for (int i = 0; i < n; i++) ends = ends && ((code->generators[i] >> (K - 1)) & 1u) && (code->generators[i] & 1u);
         vtb::Launch la;
         la.S = S, la.soft = 0, la.T = T, la.L = info_bits;
         la.in = d_in, la.in_stride = in_stride, la.out = d_out, la.out_stride = out_stride;
-        la.frames = frames, la.stream = st, la.cus = vtb::current_device_cus();
+        la.frames = frames, la.stream = st, la.cus = vtb::current_device_cus(), la.dbg = kn.dbg;
+        la.guard_hits = vtb::debug_guard_hits();
         uint32_t rg[3];
         for (int i = 0; i < 3; i++) rg[i] = vtb::gen_rev(code->generators[i], K);
         for (int j = 0; j < (1 << (K - 2)); j++) {  // label of butterfly j: the encoder on delay (j << 1) | 0 (reference :24-29)
@@ -487,9 +506,9 @@ int vtb_genk_decode_device(const vtb_genk_code_t* code, int32_t info_bits, const
     }
     vtb::GenArgs a{};
     a.k = k, a.S = S, a.n = n, a.N = N, a.T = T, a.L = info_bits, a.R = R, a.u8 = u8 ? 1 : 0;
-    a.dbg = vtb::debug_flags();
-    a.warm = 96;
-    if (const char* w = getenv("VTB_GENK_WARM")) a.warm = std::max(0, atoi(w));  // measurement only
+    a.dbg = kn.dbg;
+    a.hits = vtb::debug_guard_hits();
+    a.warm = kn.genk_warm >= 0 ? kn.genk_warm : 96;  // ($VTB_GENK_WARM: measurement only)
     for (int i = 0; i < n; i++) a.rg[i] = vtb::gen_rev(code->generators[i], k * K);
     // survivor pointers in LDS while they leave room for 4 waves per CU, else in a workspace
     const size_t dec_bytes = (vtb::gen_ptr_bytes(T, S, N) + 15) & ~size_t(15);

@@ -40,6 +40,13 @@ struct Launch {
     // not converge ([0] = count, then frame indices; decoded again by the list kernel)
     int split_warm = 96;
     uint32_t* fail_list = nullptr;
+    // the plan's knobs (Knobs above): VTB_DEBUG bits, a fixed split warm-up, the K=9 SEG grid stride
+    int dbg = 0;
+    int split_warm_force = 0;
+    int seg9_xcd = -1;
+    // Testing only (vtb_debug_set_guard_counter): a device word every traceback completeness
+    // guard that fires adds 1 to (the frame then takes its exact slow path).  Null in production.
+    uint32_t* guard_hits = nullptr;
     uint8_t symm[1 << (kMaxS - 1)] = {};
 };
 
@@ -53,16 +60,55 @@ const char* last_kernel();
 unsigned long long* debug_tstamp();
 void set_debug_tstamp(unsigned long long* p);
 
-// Measurement-only knobs from $VTB_DEBUG (bit 0: skip traceback, bit 1: skip ACS; K=7 LDS
-// kernel: bit 2 skip traceback verification, bit 3 warm-up walk only, bit 4 return at entry, bit 5
-// one wave per frame pair instead of the persistent grid, bit 6 streaming survivors in the
-// global ring only, bit 8 never split frames across the halves of a wave, bit 10 no
-// single-frame SEG kernel, bit 11 global-survivor variant without the LDS part).  Never
-// set in production; outputs are garbage when set.
-inline int debug_flags() {
-    const char* v = getenv("VTB_DEBUG");
-    return v ? atoi(v) : 0;
+// Testing and measurement knobs, read from the environment once -- when a plan or a stream
+// object is created (vtb_plan_create, vtb_stream_create; per call only for the plan-less
+// vtb_genk_decode_device) -- and carried from there into every launch (Launch::dbg ...), never
+// parsed per launch.  The reference is configured at compile time only
+// (/root/reference/src/viterbiDecoder.h:17-39); production sets none of these.
+//
+// $VTB_DEBUG bits.  Exact (output unchanged; kernel choice and forced slow paths for the tests):
+//   5 one wave per frame pair instead of the persistent grid, 6 streaming survivors in the global
+//   ring only, 8 never split frames across the halves of a wave, 10 no single-frame SEG kernel,
+//   11 global-survivor variant without its LDS part, 12 never the persistent split kernel,
+//   13 full last chunk, 14 no in-wave split fix-up, 15 fix-up on every split frame, 16 fix-up
+//   checkpoints never match, 17 traceback verification capped at one round (every kernel's
+//   completeness guard then sends each chain not yet proven to its exact slow path).
+// Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
+//   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE
+//   build (tools/build_variants.sh) honours them; the shipped library masks them off.
+constexpr int kDbgUnsafe = 0x1F;
+constexpr int kDbgTbCap = 1 << 17;
+#ifdef VTB_MEASURE
+constexpr int kDbgHonoured = ~0;
+#else
+constexpr int kDbgHonoured = ~kDbgUnsafe;
+#endif
+
+// $VTB_KERNEL: force one kernel family (testing and A/B measurement).
+enum class Force { Any, K7, Gws, K9, Lds, Seg, K7s, Genk, Unknown };
+
+struct Knobs {
+    int dbg = 0;              // $VTB_DEBUG & kDbgHonoured
+    Force force = Force::Any;
+    int split_warm = 0;       // $VTB_SPLIT_WARM: fixed split warm-up (0: chosen by occupancy)
+    int genk_warm = -1;       // $VTB_GENK_WARM (-1: 96)
+    int seg_waves = 0;        // $VTB_SEG_WAVES (0: 8, or 4 where 8 do not fit)
+    int seg_warm = 0;         // $VTB_SEG_WARM (0: kSegWarm; set: no adaptive short warm-up)
+    bool seg_adapt = true;    // $VTB_SEG_ADAPT != "0"
+    int seg9_wgs = 0;         // $VTB_SEG9_WGS (0: kSeg9Wgs)
+    int seg9_waves = 0;       // $VTB_SEG9_WAVES (0: kSeg9Waves)
+    int seg9_xcd = -1;        // $VTB_SEG9_XCD (-1: automatic)
+};
+Knobs read_knobs();
+
+// A completeness guard fired (testing counter, Launch::guard_hits; one lane calls it).
+__device__ __forceinline__ void note_guard(uint32_t* hits) {
+    if (hits) atomicAdd(hits, 1u);
 }
+
+// The guard counter of the next launches (nullptr: off).  Testing only.
+uint32_t* debug_guard_hits();
+void set_debug_guard_hits(uint32_t* p);
 
 // Resident blocks per CU of a 64-thread kernel with `lds` bytes of dynamic LDS
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor, cached: the query costs host time on every
@@ -71,12 +117,6 @@ int resident_per_cu(const void* kernel, size_t lds);
 
 // Compute units of the calling thread's current device (cached per device; 256 if unknown).
 int current_device_cus();
-
-// getenv(name) equals value.
-inline bool env_is(const char* name, const char* value) {
-    const char* v = getenv(name);
-    return v && strcmp(v, value) == 0;
-}
 
 // Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
 // shape limits are reported through *_supported() beforehand.

@@ -81,16 +81,8 @@ namespace {
 
 using namespace k7;
 
-#ifdef VTB_EXP_B128
-// measurement: rows r and r + 6 of a column adjacent (slot 12 (r / 12) + 2 (r % 6) + (r % 12) / 6),
-// so one ds_read_b128 (4 LDS cycles) replaces a ds_read2_b64 (8); 50 slots keep the column
-// bases 16-byte aligned and the eight columns of a row in distinct banks (100 dwords apart)
-constexpr int kCol = 50;
-__host__ __device__ constexpr int ring_slot(int r) { return 12 * (r / 12) + 2 * (r % 6) + (r % 12) / 6; }
-#else
 constexpr int kCol = 49;                   // 8-byte slots per table column (48 rows + bank skew)
 __host__ __device__ constexpr int ring_slot(int r) { return r; }
-#endif
 constexpr int kRingBytes = 8 * kCol * 8;   // branch-metric ring: 8 (label, R) columns
 // Rate 1/3 (NB = 3): 16 (label, R) columns of a 24-row ring (25 slots: the 16 columns of a row
 // in distinct bank pairs), refilled half a chunk at a time (k7_pair), so that the ring, 3.2 KB,
@@ -100,19 +92,16 @@ constexpr int kColN = NB == 3 ? 25 : kCol;   // 8-byte slots per table column
 template <int NB>
 constexpr int kRowsN = NB == 3 ? 24 : kChunk;  // ring rows
 constexpr int ring_bytes(int NB) { return (2 << NB) * (NB == 3 ? kColN<3> : kCol) * 8; }
-#ifndef VTB_EXP_TBWARM
-#define VTB_EXP_TBWARM 48
-#endif
-constexpr int kTbWarm = VTB_EXP_TBWARM;  // traceback warm-up steps past a block's end (multiple of 48)
+constexpr int kTbWarm = 48;  // traceback warm-up steps past a block's end (multiple of 48)
 // Share of its chunks the second-dispatched wave of a SIMD runs at priority 1 (wave balance,
 // k7_pair).  Round 2: 55 / 59 / 63 measured alike (31.06 / 31.1 / 31.0 us per 4,096-frame launch);
 // round 4, ten interleaved rounds over two boxes (profiles/r04/first/ab_prio_*.txt): 67 is
 // 0.4-0.6 % faster than 59, 50 / 71 / 75 slower.
-#ifndef VTB_EXP_PRIO
-#define VTB_EXP_PRIO 67
-#endif
-constexpr int kPrioPct = VTB_EXP_PRIO;
+constexpr int kPrioPct = 67;
 constexpr uint32_t kR1 = 0x10001u;
+// Soft renormalisation period in steps (divides the 48-step chunk).  16 would overflow the u16
+// metrics on padding rows (tests/test_metric_bounds.py).
+constexpr int kRenormSoft = 12;
 
 // History bits per u16 half: soft input keeps 4m + h (2 history bits, the
 // exact metric needs 14 bits); hard input, whose metrics stay below 128, keeps 256m + h
@@ -184,41 +173,14 @@ __host__ __device__ __forceinline__ uint32_t lane_of(uint32_t l) { return l ^ ((
 // result (one wait state each way: tools/probes/permlane_hazard.hip).
 template <int P>
 __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, uint32_t& B) {
-#ifdef VTB_EXP_NONOP
-    // measurement only (wrong results): A and B without the hazard wait states, to bound
-    // what filling them could gain (the min is fused in by step_nonop below)
-    A = m, B = vw.x ^ vw.y;
-    return;
-#endif
-#ifdef VTB_EXP_SWZ
-    // measurement only: the cross-row partners through the LDS crossbar instead of the VALU
-    // (lane XOR 16 by ds_swizzle's bit mode; with VTB_EXP_SWZ >= 2 also XOR 32 by ds_bpermute)
-    if constexpr (P == 4) {
-        A = m + vw.x;
-        B = uint32_t(__builtin_amdgcn_ds_swizzle(int(m), 0x401F)) + vw.y;
-        return;
-    }
-    if constexpr (P == 5 && VTB_EXP_SWZ >= 2) {
-        const int x32 = int((__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ^ 32u) << 2);
-        A = m + vw.x;
-        B = uint32_t(__builtin_amdgcn_ds_bpermute(x32, int(m))) + vw.y;
-        return;
-    }
-#endif
     if constexpr (P == 4 || P == 5) {
-#ifdef VTB_EXP_E32
-#define VTB_ADD_ENC "v_add_u32_e32"  // measurement: the 4-byte VOP2 encoding of the add
-#else
-#define VTB_ADD_ENC "v_add_u32"
-#endif
         if constexpr (P == 4) {
-            asm volatile(VTB_ADD_ENC " %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
+            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane16_swap_b32 %1, %1\n\ts_nop 0"
                          : "=&v"(A), "+v"(m) : "v"(vw.x));
         } else {
-            asm volatile(VTB_ADD_ENC " %0, %1, %2\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 0"
+            asm volatile("v_add_u32 %0, %1, %2\n\tv_permlane32_swap_b32 %1, %1\n\ts_nop 0"
                          : "=&v"(A), "+v"(m) : "v"(vw.x));
         }
-#undef VTB_ADD_ENC
         B = m + vw.y;
     } else {
         A = m + vw.x;
@@ -230,24 +192,10 @@ __device__ __forceinline__ void candidates(uint32_t m, uint2 vw, uint32_t& A, ui
     }
 }
 
-#ifdef VTB_EXP_SGMASK
-__device__ __forceinline__ uint32_t sg_and(uint32_t smask, uint32_t v) {
-    uint32_t r;
-    asm("v_and_b32_e32 %0, %1, %2" : "=v"(r) : "s"(smask), "v"(v));
-    return r;
-}
-#endif
-
 // One v_bfi_b32 (the compiler otherwise splits a constant-mask select into and/and/or).
 __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b) {
     uint32_t r;
-#ifdef VTB_EXP_BITOP3
-    // v_bitop3_b32 with the bit-select truth table: issues at the fast (two-pass) rate,
-    // v_bfi_b32 at the four-cycle rate (profiles/r01/isa_bench*.txt)
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
-#else
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
-#endif
     return r;
 }
 
@@ -335,19 +283,14 @@ __device__ __forceinline__ uint64_t tb_body_spec(uint32_t cb, uint32_t& l4, uint
     return bits;
 }
 
-// The serial form is the shipped one.  The speculative form (VTB_EXP_TBSPEC, measurement
-// only) measured slower where it matters: LDS words 6 % per 4,096-frame launch (2.5 random
+// The serial form is the shipped one.  The speculative form (round 1, measurement only) measured slower where it matters: LDS words 6 % per 4,096-frame launch (2.5 random
 // reads per window cost more LDS bandwidth than the latency they hide, with 8 waves per CU
 // tracing back at once), global words 2 % slower on config C3 (65,536 x 2,048 bits: the
 // extra loads queue behind other waves' traffic), 2 % faster only for one 4,096-frame round
 // with global words.
 template <bool GS>
 __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& l4, uint64_t gbase) {
-#if defined(VTB_EXP_TBSPEC)
-    return tb_body_spec<GS>(cb, l4, gbase);
-#else
     return tb_body_serial<GS>(cb, l4, gbase);
-#endif
 }
 
 __device__ __forceinline__ uint32_t rotl6c(uint32_t x, int r) { return r == 0 ? x : ((x << r) | (x >> (6 - r))) & 63u; }
@@ -450,61 +393,31 @@ __device__ __forceinline__ void put_bits48(uint8_t* ob, int tlo, uint64_t bits) 
     o[2] = (unsigned short)((rh >> 24) | ((rh >> 8) & 0xff00u));
 }
 
-// Measurement-only variants (tools/build_variants.sh builds them into separate libraries,
-// never the shipped one; their outputs are wrong): no table staging inside the ACS loop /
-// no survivor-word stores.
-#ifndef VTB_EXP_AHEAD
-#define VTB_EXP_AHEAD 2
-#endif
-#ifdef VTB_EXP_NO_TABREAD
-#define VTB_EXP_TABREAD(rd, reg) make_uint2((reg).y, (reg).x)
-#elif defined(VTB_EXP_TAB32)
-// measurement only: read V alone (4 B per lane) and derive W = (8Q + tie) - V at use
-#define VTB_EXP_TABREAD(rd, reg) make_uint2(reinterpret_cast<const uint32_t*>(&(rd))[0], 0u)
-#else
-#define VTB_EXP_TABREAD(rd, reg) (rd)
-#endif
-#ifdef VTB_EXP_TAB32
-#define VTB_EXP_VW(vw, I) make_uint2((vw).x, (8 * Q + (1u << ((I) & (H::HB - 1)))) * kR1 - (vw).x)
-#else
-#define VTB_EXP_VW(vw, I) (vw)
-#endif
-#ifdef VTB_EXP_NO_STAGE
-#define VTB_EXP_STAGE false
-#else
-#define VTB_EXP_STAGE true
-#endif
-#ifdef VTB_EXP_NO_WORD
-#define VTB_EXP_WORD(x) asm volatile("" ::"v"(z))
-#else
-#define VTB_EXP_WORD(x) x
-#endif
+// The completeness guard's slow path (k7_pair): one frame traced back serially, 48 steps per
+// walk, from location 0 at Tpad -- the reference's own walk (viterbiDecoderButterflyk1.c:
+// 200-256), exact whatever the block-parallel chains did; it runs only when a verified chain
+// is left unproven.  (Inlined: the walks' asm takes the workspace base in SGPRs.)  cb0, hyb,
+// tg, lds_off, gbase: k7_pair's traceback addressing.
+template <bool SOFT, bool GS>
+__device__ __forceinline__ void tb_serial_frame(uint8_t* ob, int Tpad, uint32_t cb0, bool hyb, int tg, uint32_t lds_off,
+                                             uint64_t gbase) {
+    uint32_t l = 0;
+    for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48) {
+        const uint32_t cb = cb0 + 256 * (tlo >> 4);
+        uint64_t bits;
+        if (GS && hyb) bits = SOFT ? tb_body_dual(cb, l, tlo >= tg, lds_off, gbase) : tb_body8_dual(cb, l, tlo >= tg, lds_off, gbase);
+        else bits = SOFT ? tb_body<GS>(cb, l, gbase) : tb_body8<GS>(cb, l, gbase);
+        put_bits48(ob, tlo, bits);
+    }
+}
 
-#ifdef VTB_EXP_NONOP
-#define VTB_EXP_ACS(P, M, vw) M = step_nonop<P>(M, vw);
-#else
-#define VTB_EXP_ACS(P, M, vw)                                                                    \
+// One ACS step of the lane's location pair: both candidates, then the packed minimum.
+#define VTB_ACS(P, M, vw)                                                                        \
     {                                                                                            \
         uint32_t A, B;                                                                           \
         candidates<P>(M, vw, A, B);                                                              \
         M = pk_min(A, B);                                                                        \
     }
-#endif
-#ifdef VTB_EXP_NONOP
-template <int P>
-__device__ __forceinline__ uint32_t step_nonop(uint32_t m, uint2 vw) {
-    uint32_t A, B;
-#define VTB_NN(X) asm volatile("v_add_u32 %1, %0, %3\n\t" X "\n\tv_pk_min_u16 %0, %1, %2" : "+v"(m), "=&v"(A), "=&v"(B) : "v"(vw.x), "v"(vw.y));
-    if constexpr (P == 5) VTB_NN("v_permlane32_swap_b32 %0, %0\n\tv_add_u32 %2, %0, %4")
-    if constexpr (P == 4) VTB_NN("v_permlane16_swap_b32 %0, %0\n\tv_add_u32 %2, %0, %4")
-    if constexpr (P == 3) VTB_NN("v_add_u32_dpp %2, %0, %4 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-    if constexpr (P == 2) VTB_NN("v_add_u32_dpp %2, %0, %4 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1")
-    if constexpr (P == 1) VTB_NN("v_add_u32_dpp %2, %0, %4 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1")
-    if constexpr (P == 0) VTB_NN("v_add_u32_dpp %2, %0, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1")
-#undef VTB_NN
-    return m;
-}
-#endif
 
 // Survivor word W (of the chunk's three) of this lane: LDS store, or a global store at
 // byte offset gvo + 256 W of the wave's workspace (one coalesced 256-B wave store).
@@ -593,7 +506,8 @@ __device__ __forceinline__ void tb_walk48_pair(uint32_t cb, uint32_t& l4a, uint3
 // from the lower of the two frames' new emission points -- are copied into the ring.
 template <bool SOFT, bool GS>
 __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
-                                 uint64_t gbase, size_t fa, bool has_b, size_t wp, uint32_t r0) {
+                                 uint64_t gbase, size_t fa, bool has_b, size_t wp, uint32_t r0, int dbg,
+                                 uint32_t* hits) {
     const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
     uint32_t* st = sa.state + wp * kStreamStateWords;
     const int e0 = int(st[64 + f]);  // this lane's frame
@@ -656,15 +570,24 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
                 }
             }
         }
-        // verification, as in the frame decoder (the last active block of a frame is known)
+        // verification, as in the frame decoder (the last active block of a frame is known; a
+        // chain of 32 blocks needs at most 31 re-walk rounds), with its completeness guard: a
+        // frame still unproven after the cap (VTB_DEBUG bit 17: one round) is walked serially
+        // from its known location at hi by lane 32f
         uint32_t fin = loc;
         bool fixed = known || !active;
-        for (int round = 0; round < 33; round++) {
+        const int rounds = (dbg & kDbgTbCap) ? 1 : 33;
+        bool unproven = false;
+        for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
             const bool ok = fixed || loc_top == sf;
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0) break;
+            if (round == rounds) {
+                unproven = true;
+                break;
+            }
             const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
             if (!ok && succ_proven) {
                 loc = sf;
@@ -675,6 +598,11 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
                 fin = loc;
                 fixed = true;
             }
+        }
+        if (unproven && blk == 0) {
+            note_guard(hits);
+            uint32_t l = kloc;
+            for (int tlo = hi - 48; tlo >= e0; tlo -= 48) put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, l));
         }
     }
     const int bits_out = lost ? -1 : sa.last ? T - 6 - e0 : hi - e0;
@@ -895,9 +823,6 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // first: no survivor stores outstanding.  In the loop (GS) one survivor-word store (step
     // 15 of the chunk) was issued after the loads; vmcnt retires in issue order.
     auto stage_compute = [&](uint32_t ra, uint32_t rb, uint32_t (&e)[NL], uint32_t (&et)[NL], bool first) {
-#ifdef VTB_EXP_RAWNOWAIT
-        ra = lane * 0x0101u, rb = lane * 0x0303u;  // measurement only: no wait for the loads
-#else
         if constexpr (SEG) {
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
         } else if (GS && !first) {
@@ -905,7 +830,6 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         } else {
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
         }
-#endif
         // packed [frame A, frame B] received values of coded bits 0 and 1, times four
         uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
         uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u), q2 = 0;
@@ -977,17 +901,9 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #define VTB_W2(base, k, v, w)                                                                         \
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
                  "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
-#ifdef VTB_EXP_STAGE48
-        // measurement: lanes 48-63 (duplicates of rows 0-15) skip the staging writes, so the
-        // second 32-lane group of each write has no two lanes on one bank (round 4 LDS-conflict A/B)
-        if (lane < kChunk) {
-#endif
         VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
         VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
         VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
-#ifdef VTB_EXP_STAGE48
-        }
-#endif
 #undef VTB_W2
         if (SEG) {
             // either half may hold padding rows (steps >= Ta in A, >= Tb in B): own-keeping rows
@@ -1070,7 +986,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // software pipeline: the table pairs of group G+3 are read while group G computes, into
     // the slot of a four-group register ring (8 groups per chunk: no copies at the loop edge)
     uint2 buf[4][6];
-    constexpr int AH = VTB_EXP_AHEAD;  // groups read ahead (2 or 3)
+    constexpr int AH = 2;  // groups read ahead
     auto prime = [&]() {  // the first AH groups' table pairs of a freshly staged chunk
 #pragma unroll
         for (int g = 0; g < AH; g++)
@@ -1090,10 +1006,6 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     const uint32_t widx = rev6(lane_of(lane));  // survivor word slot of this lane's location
 
     uint32_t dd = 0, m_prev = 0, pw[4] = {0, 0, 0, 0};
-#ifdef VTB_EXP_SGMASK
-    uint32_t clr_mask;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(clr_mask) : "i"(~H::MASK));
-#endif
     const int tacs = (dbg & 2) ? 0 : (SPLIT && sp ? t1s : Tpad);
     // One 48-step chunk of the ACS (fully unrolled); PADTAG: this chunk stages the chunk that
     // holds step T (padding rows possible).
@@ -1106,44 +1018,31 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         constexpr bool GSC = decltype(gtag)::value;
         constexpr bool LASTC = decltype(lasttag)::value;
         const int c0 = t0 / kChunk;
-#ifdef VTB_EXP_B128
-        const uint2* ap[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) ap[k] = reinterpret_cast<const uint2*>(tab + off[k]);
-#else
         LdsCol ap[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) ap[k].a = tad[k];
-#endif
         uint32_t* dchunk = dec + ((t0 - lds_t0) >> 4) * 64 + widx;  // (LDS words; stream: this call's)
         // GS: byte offset of the lane's words (streaming: position in the survivor ring)
         const uint32_t gvo = 4u * (((STREAM ? t0 % sa.ring : t0) >> 4) * 64 + widx);
 
 // Renormalisation: reference = location 0 (lane 0) at a step whose history is clear, the
 // subtraction folded into the history clear (soft: every 12 steps; hard: once per chunk).
-#ifndef VTB_EXP_RN
-#define VTB_EXP_RN 12  // soft renormalisation period in steps (12, 16 or 24: divides the chunk)
-#endif
-#define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)
-#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)
+#define VTB_RENORM_READ(I) (SOFT ? ((I) % kRenormSoft) == kRenormSoft - 2 : (I) == 40)
+#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % kRenormSoft) == kRenormSoft - 1 : (I) == 47)
 // (SPLIT fix-up pass: frame B's 16-bit half of the word only, frame A's stays)
 #define VTB_STORE(GSC_, W_, z_)                                                                   \
     {                                                                                            \
         if (SPLIT && fixp) reinterpret_cast<uint16_t*>(dchunk + (W_) * 64)[1] = uint16_t((z_) >> 16); \
         else store_word<GSC_>(dchunk, gvo, gbase, (W_), (z_));                                   \
     }
-#ifdef VTB_EXP_SGMASK
-#define VTB_CLR(x) sg_and(clr_mask, (x))  // measurement: the clear mask from an SGPR, no literal
-#else
 #define VTB_CLR(x) ((x) & ~H::MASK)
-#endif
 #define VTB_STEP(I, PH)                                                                          \
     {                                                                                            \
         if (VTB_RENORM_READ(I)) {                                                                \
             const uint32_t ref = __builtin_amdgcn_readfirstlane(M);                              \
             asm("s_sub_u32 %0, %1, %2" : "=s"(dd) : "s"(H::BIAS * kR1), "s"(ref) : "scc");       \
         }                                                                                        \
-        VTB_EXP_ACS(5 - (PH), M, VTB_EXP_VW(cur[PH], I))                                         \
+        VTB_ACS(5 - (PH), M, cur[PH])                                                            \
         if (SOFT && ((I) & 1)) {                                                                 \
             /* window (I) >> 1 & 7 of the word: history bytes of two windows by one v_perm */    \
             const int w = ((I) & 15) >> 1;                                                       \
@@ -1155,7 +1054,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 uint32_t z = bfi_op(0x03030303u, pw[0], pw[1] << 2);                             \
                 z = bfi_op(0x0F0F0F0Fu, z, pw[2] << 4);                                          \
                 z = bfi_op(0x3F3F3F3Fu, z, pw[3] << 6);                                          \
-                VTB_EXP_WORD(VTB_STORE(GSC, (I) >> 4, z));                                      \
+                VTB_STORE(GSC, (I) >> 4, z);                                                     \
             }                                                                                    \
         }                                                                                        \
         if (!SOFT && ((I) & 7) == 7) {                                                           \
@@ -1164,7 +1063,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
                 m_prev = M;                                                                      \
             } else {                                                                             \
                 const uint32_t z = __builtin_amdgcn_perm(M, m_prev, 0x06020400u);                \
-                VTB_EXP_WORD(VTB_STORE(GSC, (I) >> 4, z));                                      \
+                VTB_STORE(GSC, (I) >> 4, z);                                                     \
             }                                                                                    \
             M = VTB_RENORM_APPLY(I) ? (VTB_CLR(M) + dd) : VTB_CLR(M);                            \
         }                                                                                        \
@@ -1172,11 +1071,11 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 #define VTB_GROUP(G)                                                                              \
     if (!LASTC || (G) < ng_last) {                                                                \
         if ((G) == 0 && !LASTC) load_raw(c0 + 1, ra, rb);                                         \
-        if ((G) == 3 && VTB_EXP_STAGE && !LASTC) stage_compute(ra, rb, se, set, !GSC);            \
-        if ((G) == 8 - AH && VTB_EXP_STAGE && !LASTC) { /* all rows of this chunk are in registers */ \
+        if ((G) == 3 && !LASTC) stage_compute(ra, rb, se, set, !GSC);            \
+        if ((G) == 8 - AH && !LASTC) { /* all rows of this chunk are in registers */ \
             stage_write(c0 + 1, se, set, padtag);                                                 \
         }                                                                                         \
-        if (NB == 3 && (G) == 1 && VTB_EXP_STAGE) { /* rows 24-47 of this chunk: rows 0-23 are read */ \
+        if (NB == 3 && (G) == 1) { /* rows 24-47 of this chunk: rows 0-23 are read */ \
             stage_write(c0, se, set, std::true_type{}, 1);                                       \
         }                                                                                         \
         uint2* cur = buf[(G) & 3];                                                                \
@@ -1186,28 +1085,14 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
         VTB_STEP(6 * (G) + 2, 2) VTB_STEP(6 * (G) + 3, 3)                                         \
         VTB_STEP(6 * (G) + 4, 4) VTB_STEP(6 * (G) + 5, 5)                                         \
     }
-#if !defined(VTB_EXP_RD1) && !defined(VTB_EXP_NO_TABREAD) && !defined(VTB_EXP_TAB32) && VTB_EXP_AHEAD == 2
 // Even groups read the next two groups' pairs of one phase (rows 6 apart in one column of
 // the ring): one ds_read2_b64 per phase and group pair, half the LDS read instructions of
-// one ds_read_b64 per step (measured 2% faster).  (VTB_EXP_RD1: one read per step.)
-#ifdef VTB_EXP_B128
-#define VTB_RD(G, k)                                                                              \
-    if (((G) & 1) == 0) {                                                                         \
-        const uint4 q_ = reinterpret_cast<const uint4*>(ap[k])[ring_slot((6 * ((G) + 2) + (k)) % kChunk) / 2]; \
-        buf[((G) + 2) & 3][k] = make_uint2(q_.x, q_.y);                                           \
-        buf[((G) + 3) & 3][k] = make_uint2(q_.z, q_.w);                                           \
-    }
-#else
+// one ds_read_b64 per step (measured 2% faster).
 #define VTB_RD(G, k)                                                                              \
     if (((G) & 1) == 0) {                                                                         \
         buf[((G) + 2) & 3][k] = ap[k][(6 * ((G) + 2) + (k)) % kChunk % kRowsN<NB>];               \
         buf[((G) + 3) & 3][k] = ap[k][(6 * ((G) + 3) + (k)) % kChunk % kRowsN<NB>];               \
     }
-#endif
-#else
-#define VTB_RD(G, k)                                                                              \
-    buf[((G) + AH) & 3][k] = VTB_EXP_TABREAD(ap[k][(6 * ((G) + AH) + (k)) % kChunk % kRowsN<NB>], buf[(G) & 3][k]);
-#endif
         VTB_GROUP(0) VTB_GROUP(1) VTB_GROUP(2) VTB_GROUP(3) VTB_GROUP(4) VTB_GROUP(5) VTB_GROUP(6) VTB_GROUP(7)
 #undef VTB_GROUP
 #undef VTB_STEP
@@ -1224,9 +1109,6 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // launch -3.5 %).  Scheduling only: decisions are unchanged.
     uint32_t hwid;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-#ifdef VTB_EXP_NOPRIO
-    hwid = 0;  // measurement only: age arbitration
-#endif
     const bool second = (hwid & 1u) != 0;
     const int hi_chunks = kPrioPct * ((tacs - tbeg) / kChunk) / 100;
     auto prio = [&](int t0) {
@@ -1328,7 +1210,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     tstamp(table, 1);
     if constexpr (STREAM) {
         if (!sa.last) sa.state[wp * kStreamStateWords + lane] = M;
-        stream_traceback<SOFT, GS>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, uint32_t(r0));
+        stream_traceback<SOFT, GS>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, uint32_t(r0), dbg, table.guard_hits);
         return;
     }
     const size_t units = SPLIT ? frames : (frames + 1) / 2;  // (persistent loop: pairs, or split frames)
@@ -1451,21 +1333,32 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // a re-walk can change their exit, so the checks repeat until every block is proven --
     // one round when all blocks merged within the warm-up.
     // Rounds: every round proves at least the last unproven block of each chain (its successor
-    // is proven), so a chain of n blocks needs at most n rounds plus the one that sees no
-    // failure.  Unsplit frames are chains of at most 32 blocks; the split pass chains frame A's
-    // nA <= 32 blocks and frame B's blocks 2..31 into one chain of up to 62.  (Round 3 capped
-    // this loop at 33 rounds for both: a pure-noise split frame kept by the in-wave fix-up left
-    // frame A's first blocks unverified -- fuzz case 1366, 6 wrong bits at 85-93, DESIGN.md
-    // 4.2b.)  With 65 rounds no block can leave the loop unproven.
+    // is proven; the chain's last block is known), so a chain of n blocks needs at most n - 1
+    // re-walk rounds plus the check that sees no failure.  Unsplit frames are chains of at most
+    // 32 blocks; the split pass chains frame A's nA <= 32 blocks and frame B's blocks kB0..31
+    // (kB0 = 32 + warm / 48 >= 33 for warm >= 48) into one chain of nA + 64 - kB0 <= 63.  (Round
+    // 3 capped this loop at 33 rounds for both: a pure-noise split frame kept by the in-wave
+    // fix-up left frame A's first blocks unverified -- fuzz case 1366, 6 wrong bits at 85-93,
+    // DESIGN.md 4.2b.)
+    // Completeness guard (round 5): the loop's last check runs after the cap's re-walks, and a
+    // block still unproven there never reaches the output -- the split pass sends its frame to
+    // the slow path (the unsplit pass, or the list kernel), an unsplit frame is traced back
+    // serially from location 0 at Tpad (the reference's own walk, viterbiDecoderButterflyk1.c:
+    // 200-256).  VTB_DEBUG bit 17 caps the loop at one re-walk round to exercise both.
     uint32_t fin = loc;  // survivor's location at step blk * tbb
-    bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement only): skip verification
-    const int rounds = (SPLIT && sp) ? 65 : 33;
-    for (int round = 0; round < rounds; round++) {
+    bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement builds only): skip verification
+    const int rounds = (dbg & kDbgTbCap) ? 1 : (SPLIT && sp) ? 65 : 33;
+    uint64_t unproven = 0;
+    for (int round = 0;; round++) {
         // successor's exit (lane 31, frame A's last block, is known)
         const uint32_t sf = (SPLIT && sp) ? __shfl(fin, lane == nA - 1 ? kB0 : (lane + 1) & 63) : __shfl_down(fin, 1);
         const bool ok = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
+        if (round == rounds) {
+            unproven = bad;
+            break;
+        }
         bool succ_proven;
         if (SPLIT && sp) {  // one chain: frame A's blocks 0..nA-1, then frame B's blocks 2..31
             const uint64_t cm = (bad & ((uint64_t(1) << nA) - 1)) | ((bad >> kB0) << nA);
@@ -1484,6 +1377,23 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             fin = loc;
             fixed = true;
         }
+    }
+    if (unproven) {
+        if (lane == 0) note_guard(table.guard_hits);
+        if (SPLIT && sp) {
+            if constexpr (LOOP) {  // the list kernel decodes the frame afterwards
+                if (lane == 0) {
+                    const uint32_t i = atomicAdd(table.fail_list, 1u);
+                    table.fail_list[1 + i] = uint32_t(fa);
+                }
+                if (!GS && next < units) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pra), "+v"(prb));
+                return;
+            } else {
+                continue;  // pass 1: the frame unsplit
+            }
+        }
+        // an unsplit frame with an unproven block: lane 32f walks frame f whole
+        if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) tb_serial_frame<SOFT, GS>(ob, Tpad, cb0, hyb, tg, lds_off, gbase);
     }
     __syncthreads();
     tstamp(table, 2);
@@ -1521,11 +1431,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
 // CUs hold in one round and for the streaming decoder (the loop's extra live state costs
 // ~3 % there).  GS: survivor slot = the wave (streaming: the pair, whose ring persists).
 template <bool SOFT, bool GS, bool STREAM, bool LOOP, bool SPLIT = false, bool LIST = false, int NB = 2>
-#ifdef VTB_EXP_WPE
-#define VTB_K7_WPE __attribute__((amdgpu_waves_per_eu(1, VTB_EXP_WPE)))
-#else
 #define VTB_K7_WPE
-#endif
 __global__ __launch_bounds__(64) VTB_K7_WPE void k7_lds_kernel(const uint8_t* __restrict__ in, size_t in_stride,
                                                     uint8_t* __restrict__ out, size_t out_stride, int T, int L,
                                                     int Tpad, int tbb, int r0, size_t frames, int dbg, Launch table,
@@ -1671,13 +1577,22 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
             }
         }
     }
+    // one chain of up to 64 blocks (at most 63 re-walk rounds), with the completeness guard:
+    // unproven after the cap (VTB_DEBUG bit 17: one round), lane 0 walks the frame serially
+    // from location 0 at Tpad
     uint32_t fin = loc;
     bool fixed = known || !active;
-    for (int round = 0; round < 65; round++) {
+    const int rounds = (dbg & kDbgTbCap) ? 1 : 65;
+    bool unproven = false;
+    for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
         const bool okb = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
+        if (round == rounds) {
+            unproven = true;
+            break;
+        }
         if (!okb && (bad >> (lane + 1)) == 0) {
             loc = sf;
             for (int g = kTbWarm / 48; g < nbody; g++) {
@@ -1687,6 +1602,11 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
             fin = loc;
             fixed = true;
         }
+    }
+    if (unproven && lane == 0) {
+        note_guard(table.guard_hits);
+        uint32_t l = 0;
+        for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48) put_bits48(ob, tlo, tb48(col_at(tlo), l));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1714,19 +1634,20 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
 // lane, so the LDS lanes gained nothing while every window paid for both loads: C3 soft
 // 1.16-1.17 vs 1.07 ms (profiles/r02/hybrid_survivors_ab.txt).  VTB_DEBUG bit 11
 // (measurement only): none.
-int gs_lds_steps(int T, bool soft) {
-    if (soft || (debug_flags() & 2048)) return 0;
+int gs_lds_steps(const Launch& a) {
+    const int T = a.T;
+    if (a.soft || (a.dbg & 2048)) return 0;
     const int per_wave = 160 * 1024 / 8 - region0(T);
     int s = per_wave > 0 ? per_wave / 16 / kChunk * kChunk : 0;
     return s < t_pad(T) ? s : t_pad(T);
 }
 // LDS of the survivor-in-global variant: table ring, decoded bytes and the newest steps' words.
-size_t lds_bytes_gs(int T, bool soft) { return (size_t)region0(T) + 16 * (size_t)gs_lds_steps(T, soft); }
+size_t lds_bytes_gs(const Launch& a) { return (size_t)region0(a.T) + 16 * (size_t)gs_lds_steps(a); }
 size_t ws_wave_bytes(int T) { return 16 * (size_t)t_pad(T); }
 constexpr size_t kMaxWsBytes = size_t(1) << 30;  // survivor workspace cap (global variant)
 
 template <bool GS>
-size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a.T, a.soft) : lds_bytes(a.T); }
+size_t lds_of(const Launch& a) { return GS ? lds_bytes_gs(a) : lds_bytes(a.T); }
 
 template <bool GS, bool LOOP = true, bool SPLIT = false>
 auto kernel_of(const Launch& a) {
@@ -1744,8 +1665,8 @@ size_t grid_waves(const Launch& a) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(lds));
     size_t grid = pairs;
-    const int per_cu = (debug_flags() & 32) ? 0  // VTB_DEBUG bit 5 (measurement only): one wave per pair
-                                             : resident_per_cu(reinterpret_cast<const void*>(kern), lds);
+    const int per_cu = (a.dbg & 32) ? 0  // VTB_DEBUG bit 5 (testing): one wave per pair
+                                     : resident_per_cu(reinterpret_cast<const void*>(kern), lds);
     if (per_cu > 0) {
         const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
         if (resident < grid) grid = resident;
@@ -1770,7 +1691,7 @@ hipError_t launch_k7(const Launch& a) {
     // Batches the CUs hold at one frame per wave (up to 2 per SIMD at L = 1024) run split
     // (one frame per wave, both halves at once: k7_pair SPLIT): twice the waves, about half
     // the dependent steps per wave.  VTB_DEBUG bit 8 (measurement only): never split.
-    if (!GS && a.T >= 240 && split_t1(a.T) <= 32 * kChunk && !(debug_flags() & 256)) {
+    if (!GS && a.T >= 240 && split_t1(a.T) <= 32 * kChunk && !(a.dbg & 256)) {
         auto ks = kernel_of<false, false, true>(a);
         const int per_cu = resident_per_cu(reinterpret_cast<const void*>(ks), lds);
         if (per_cu > 0 && a.frames <= size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1)) {
@@ -1786,9 +1707,9 @@ hipError_t launch_k7(const Launch& a) {
         if (e != hipSuccess) return e;
     }
     Launch la = a;
-    la.gs_steps = GS ? t_pad(a.T) - gs_lds_steps(a.T, a.soft) : (1 << 30);
+    la.gs_steps = GS ? t_pad(a.T) - gs_lds_steps(a) : (1 << 30);
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), la,
+                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, a.dbg, la,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(a.T), StreamArgs());
     return hipGetLastError();
 }
@@ -1800,8 +1721,8 @@ hipError_t launch_k7(const Launch& a) {
 // 96 steps when 8 waves per CU still fit, else 48.
 bool split_loop_params(const Launch& a, int& warm, size_t& lds) {
     if (a.S != 6 || a.T < 240) return false;
-    if (const char* v = getenv("VTB_SPLIT_WARM")) {  // measurement only: a fixed warm-up, any occupancy
-        warm = atoi(v) / kChunk * kChunk;
+    if (a.split_warm_force > 0) {  // $VTB_SPLIT_WARM (measurement only): a fixed warm-up, any occupancy
+        warm = a.split_warm_force / kChunk * kChunk;
         lds = size_t(region0(a.T)) + 16 * size_t(split_t1(a.T, warm));
         return warm >= kChunk && split_t1(a.T, warm) <= 32 * kChunk && lds <= 160 * 1024;
     }
@@ -1849,20 +1770,20 @@ hipError_t launch_k7_split_loop(const Launch& a) {
     if (grid > a.frames) grid = a.frames;
     note_kernel("k7_split_loop");
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride, a.T,
-                       a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, debug_flags(), la, nullptr, size_t(0),
+                       a.L, t_pad(a.T), tb_block(a.T), region0(a.T), a.frames, a.dbg, la, nullptr, size_t(0),
                        StreamArgs());
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // the frames that did not split: the persistent global-survivor kernel over the list (it
     // reads the count on the device; with an empty list every wave exits at once)
     auto lk = a.soft ? k7_lds_kernel<true, true, false, true, false, true> : k7_lds_kernel<false, true, false, true, false, true>;
-    const size_t llds = lds_bytes_gs(a.T, a.soft);
+    const size_t llds = lds_bytes_gs(a);
     if (llds > 64 * 1024) {
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(lk), hipFuncAttributeMaxDynamicSharedMemorySize, int(llds));
         if (e != hipSuccess) return e;
     }
-    la.gs_steps = t_pad(a.T) - gs_lds_steps(a.T, a.soft);
+    la.gs_steps = t_pad(a.T) - gs_lds_steps(a);
     hipLaunchKernelGGL(lk, dim3(unsigned(list_grid(a))), dim3(64), llds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), size_t(0), debug_flags(), la,
+                       a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T), size_t(0), a.dbg, la,
                        static_cast<uint8_t*>(a.ws) + split_list_bytes(a.frames), ws_wave_bytes(a.T), StreamArgs());
     return hipGetLastError();
 }
@@ -1896,12 +1817,12 @@ hipError_t launch_k7_lds_n3(const Launch& a) {
     const bool lp = grid < pairs;
     note_kernel(lp ? "k7_lds_n3_loop" : "k7_lds_n3");
     hipLaunchKernelGGL(lp ? loop : once, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
-                       a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T, 3), a.frames, debug_flags(), a,
+                       a.out_stride, a.T, a.L, t_pad(a.T), tb_block(a.T), region0(a.T, 3), a.frames, a.dbg, a,
                        static_cast<uint8_t*>(nullptr), size_t(0), StreamArgs());
     return hipGetLastError();
 }
 
-bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a.T, a.soft) <= 160 * 1024; }
+bool k7_global_supported(const Launch& a) { return a.S == 6 && a.T > a.S && lds_bytes_gs(a) <= 160 * 1024; }
 
 size_t k7_global_workspace_bytes(const Launch& a) { return grid_waves<true>(a) * ws_wave_bytes(a.T); }
 
@@ -1954,7 +1875,7 @@ hipError_t launch_k7_seg(const Launch& a, int waves, int warm, uint32_t* done) {
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     note_kernel("k7_seg");
     hipLaunchKernelGGL(kern, dim3(unsigned(a.frames)), dim3(64 * W), lds, a.stream, a.in, a.in_stride, a.out,
-                       a.out_stride, a.T, a.L, Tpad, r0, debug_flags(), a, sg);
+                       a.out_stride, a.T, a.L, Tpad, r0, a.dbg, a, sg);
     return hipGetLastError();
 }
 
@@ -1969,14 +1890,14 @@ hipError_t launch_k7_stream(const Launch& a, const StreamArgs& s) {
     // steps carried over from earlier calls; longer calls keep every word in the ring.
     const size_t r0 = (kRingBytes + 255) / 256 * 256;
     const size_t lds_l = r0 + 16 * size_t(s.t_end - s.t_begin);
-    const bool in_lds = lds_l <= (160 * 1024) / 8 && !(debug_flags() & 64);  // VTB_DEBUG bit 6: ring only
+    const bool in_lds = lds_l <= (160 * 1024) / 8 && !(a.dbg & 64);  // VTB_DEBUG bit 6: ring only
     auto kern = in_lds ? (a.soft ? k7_lds_kernel<true, false, true, false> : k7_lds_kernel<false, false, true, false>)
                        : (a.soft ? k7_lds_kernel<true, true, true, false> : k7_lds_kernel<false, true, true, false>);
     const size_t lds = in_lds ? lds_l : r0;
     const size_t waves = (a.frames + 1) / 2;
     note_kernel("k7_stream");
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out, a.out_stride,
-                       a.T, a.L, s.t_end, 0, int(r0), a.frames, 0, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring),
+                       a.T, a.L, s.t_end, 0, int(r0), a.frames, a.dbg, a, static_cast<uint8_t*>(a.ws), 16 * size_t(s.ring),
                        s);
     return hipGetLastError();
 }

@@ -63,12 +63,8 @@ using k7::uniform64;
 constexpr int kCh = 48;                  // ACS steps per unrolled chunk (multiple of 8 and 16)
 constexpr int kCol = 49;                 // 8-byte slots per table column (48 rows + bank skew)
 constexpr int kRingBytes = 8 * kCol * 8;  // branch-metric ring: 8 (label, R) columns
-#ifndef VTB_EXP_K9AH
-#define VTB_EXP_K9AH 2
-#define VTB_EXP_K9RS 3
-#endif
-constexpr int kAH = VTB_EXP_K9AH;        // table rows read this many steps ahead
-constexpr int kRS = VTB_EXP_K9RS;        // register ring slots (48 % kRS == 0)
+constexpr int kAH = 2;                  // table rows read this many steps ahead
+constexpr int kRS = 3;                  // register ring slots (48 % kRS == 0)
 constexpr int kTbWarm = 48;              // traceback warm-up steps past a block's end
 constexpr uint32_t kR1 = 0x10001u;
 constexpr int kColBytes = 1024;          // survivor column: 256 words per 16 steps
@@ -114,21 +110,10 @@ __device__ __forceinline__ uint32_t bfi_op(uint32_t mask, uint32_t a, uint32_t b
 // (sc1), the words another workgroup reads in the same launch (k9_seg_kernel).
 template <int OFF, bool SC = false>
 __device__ __forceinline__ void gstore(uint32_t vo, uint32_t z, uint64_t base) {
-#ifdef VTB_EXP_K9_NOWORD
-    // measurement only (wrong results): the survivor words are formed but never stored, to bound
-    // what keeping them on the CU could save; run with VTB_DEBUG=1 (no traceback)
-    asm volatile("" ::"v"(vo), "v"(z), "s"(base));
-    return;
-#endif
     if constexpr (SC)
         asm volatile("global_store_dword %0, %1, %2 offset:%3 sc1" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
-#ifdef VTB_EXP_K9_NT
-    else  // measurement: survivor words stored non-temporal (streaming L2 policy)
-        asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
-#else
     else
         asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(vo), "v"(z), "s"(base), "i"(OFF) : "memory");
-#endif
 }
 
 // Words handed from one workgroup to another inside a launch: global (never flat) agent-scope
@@ -160,15 +145,6 @@ __device__ __forceinline__ void candidates(uint32_t (&M)[4], const uint2 (&vw)[4
     } else if constexpr (P == 5 || P == 4) {
         // The adds separate the last VALU write of each M[r] from its swap; the s_nop the
         // last swap from the first read of a result (one wait state each way).
-#ifdef VTB_EXP_K9_NOSWAP
-        // measurement only (wrong results): plain moves instead of the swaps, to price them
-        asm volatile(
-            "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"
-            "v_mov_b32 %4, %4\n\tv_mov_b32 %5, %5\n\tv_mov_b32 %6, %6\n\tv_mov_b32 %7, %7"
-            : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3]), "+v"(M[0]), "+v"(M[1]), "+v"(M[2]), "+v"(M[3])
-            : "v"(vw[0].x), "v"(vw[1].x), "v"(vw[2].x), "v"(vw[3].x));
-        if constexpr (false)
-#endif
         if constexpr (P == 5) {
             asm volatile(
                 "v_add_u32 %0, %4, %8\n\tv_add_u32 %1, %5, %9\n\tv_add_u32 %2, %6, %10\n\tv_add_u32 %3, %7, %11\n\t"
@@ -209,35 +185,6 @@ template <bool SC = false>
 __device__ __forceinline__ uint64_t tb_body(uint32_t cb, uint32_t& la, uint64_t gbase) {
     uint32_t a = cb | la;
     uint64_t bits = 0;
-#ifdef VTB_EXP_TBSPEC
-    // Measurement only (1 % slower per 4,096-frame soft launch): two windows per dependent
-    // load, as vtb_k7_lds.hip tb_body_spec.
-#pragma unroll
-    for (int j = 0; j < 24; j += 2) {
-        const int todd = 47 - 2 * j, todd1 = todd - 2;
-        if (j % 4 == 0) bits |= uint64_t(lprime_of(a)) << (8 * (5 - j / 4));  // octet ending at tlo + todd + 1
-        const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
-        const int wi1 = (todd1 & 15) >> 1, sh1 = 8 * (wi1 & 1) + 2 * (wi1 >> 1);
-        const int pos = addr_pos((todd - 1) & 7), pos1 = addr_pos((todd1 - 1) & 7);
-        const uint32_t base = a & ~(3u << pos);
-        const int o = (todd >> 4) * kColBytes, o1 = (todd1 >> 4) * kColBytes, d = 1 << pos;
-        uint32_t v, c0, c1, c2, c3;
-        asm volatile(
-            "global_load_ushort %0, %5, %7 offset:%8\n\t"
-            "global_load_ushort %1, %6, %7 offset:%9\n\tglobal_load_ushort %2, %6, %7 offset:%10\n\t"
-            "global_load_ushort %3, %6, %7 offset:%11\n\tglobal_load_ushort %4, %6, %7 offset:%12\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(v), "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
-            : "v"(a), "v"(base), "s"(gbase), "i"(o), "i"(o1), "i"(o1 + d), "i"(o1 + 2 * d), "i"(o1 + 3 * d));
-        const uint32_t f = (v >> sh) & 3u;
-        a = base | (f << pos);
-        const uint32_t lo = (f & 1u) ? c1 : c0, hi = (f & 1u) ? c3 : c2;
-        const uint32_t v1 = (f & 2u) ? hi : lo;
-        a = (a & ~(3u << pos1)) | (((v1 >> sh1) & 3u) << pos1);
-    }
-    la = a & 0x3FCu;
-    return bits;
-#endif
 #pragma unroll
     for (int j = 0; j < 24; j++) {
         const int todd = 47 - 2 * j;
@@ -355,7 +302,7 @@ __device__ __forceinline__ void tb_walk48_x8(uint32_t cb, uint32_t (&la)[8], uin
 // -1 bits until last.
 template <bool SOFT>
 __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out_stride, int T, int t_end,
-                                  uint64_t gbase, size_t fa, bool has_b, size_t wp) {
+                                  uint64_t gbase, size_t fa, bool has_b, size_t wp, int dbg, uint32_t* hits) {
     const int lane = threadIdx.x, f = lane >> 5, blk = lane & 31;
     uint32_t* st = sa.state + wp * kStreamStateWords9;
     const int e0 = int(st[256 + f]);
@@ -417,14 +364,23 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
                 }
             }
         }
+        // (chains of 32 blocks: at most 31 re-walk rounds) completeness guard: a frame still
+        // unproven after the cap (VTB_DEBUG bit 17: one round) is walked serially from its known
+        // location at hi by lane 32f
         uint32_t fin = loc;
         bool fixed = known || !active;
-        for (int round = 0; round < 33; round++) {
+        const int rounds = (dbg & kDbgTbCap) ? 1 : 33;
+        uint64_t unproven = 0;
+        for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
             const bool ok = fixed || loc_top == sf;
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0 && uint32_t(bad >> (32 * (1 - f))) == 0) break;
+            if (round == rounds) {
+                unproven = bad;
+                break;
+            }
             const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
             if (!ok && succ_proven) {
                 loc = sf;
@@ -435,6 +391,11 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
                 fin = loc;
                 fixed = true;
             }
+        }
+        if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) {
+            note_guard(hits);
+            uint32_t l = kloc;
+            for (int tlo = hi - 48; tlo >= e0; tlo -= 48) put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, l));
         }
     }
     const int bits_out = lost ? -1 : sa.last ? T - 8 - e0 : hi - e0;
@@ -482,7 +443,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                                         size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
                                         size_t frames, int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t wp,
                                         size_t slot, const uint32_t (&off)[4][8], const StreamArgs& sa = StreamArgs(),
-                                        const Seg9* sg = nullptr, uint32_t* seg_out = nullptr) {
+                                        const Seg9* sg = nullptr, uint32_t* seg_out = nullptr, uint32_t* hits = nullptr) {
     static_assert(NB == 2 || (!SOFT && !STREAM && !SEG), "rate 1/3: the hard frame kernel only");
     constexpr uint32_t Q = SOFT ? 255 : 1;
     constexpr int NL = 1 << NB;  // edge labels
@@ -662,20 +623,8 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     // T - 1 hold each location's own even decision (bit 0 of each half), kept in msave for the
     // survivor fix-up below (the ACS of step T may carry another location's bit 0 into l)
     const int tsave = (STREAM && SOFT && sa.last && (T & 1)) ? T - 1 : -1;
-#ifdef VTB_EXP_K9PRIO
-    // measurement: the K=7 kernel's wave balance (vtb_k7_lds.hip kPrioPct): the second-dispatched
-    // wave of a SIMD (HW_ID wave slot 1) at priority 1 for the first VTB_EXP_K9PRIO % of its chunks
-    uint32_t hwid9;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid9));
-    const bool second9 = !SEG && (hwid9 & 1u) != 0;
-    const int hi9 = VTB_EXP_K9PRIO * ((tacs - tbeg) / kCh) / 100;
-#endif
     for (int t0 = tbeg; t0 < tacs; t0 += kCh) {
         const int c0 = t0 / kCh;
-#ifdef VTB_EXP_K9PRIO
-        if (second9 && (t0 - tbeg) / kCh < hi9) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-#endif
         // survivor column of step t0 (streaming: position in the ring)
         const uint32_t gvo = uint32_t(kColBytes) * uint32_t((STREAM ? t0 % sa.ring : t0) >> 4) + wlane;
         static_for(std::make_integer_sequence<int, kCh>{}, [&](auto ic) {
@@ -685,11 +634,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             if constexpr (I == 20) {
                 // one survivor store batch (step 15) was issued after the loads (SEG: LDS loads)
                 if constexpr (SEG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb));
-#ifdef VTB_EXP_K9_NOWORD
-                else asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra), "+v"(rb));
-#else
                 else asm volatile("s_waitcnt vmcnt(4)" : "+v"(ra), "+v"(rb));
-#endif
                 stage_compute(ra, rb, se, set);
             }
             if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);  // all rows of this chunk read
@@ -762,9 +707,6 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
                 for (int r = 0; r < 4; r++) msave[r] = M[r];
         }
     }
-#ifdef VTB_EXP_K9PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     if constexpr (SEG) {
@@ -835,7 +777,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (dbg & 1) return;
-        stream_traceback9<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp);
+        stream_traceback9<SOFT>(sa, out, out_stride, T, Tpad, gbase, fa, has_b, wp, dbg, hits);
         return;
     }
     // Soft input, padding steps [Tq, Tpad): overwrite their survivor bits with own-keeping
@@ -886,13 +828,23 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
         }
     }
+    // (chains of 32 blocks, the last known: at most 31 re-walk rounds.)  Completeness guard:
+    // a frame with a block still unproven after the cap (VTB_DEBUG bit 17: one round) is traced
+    // back serially by lane 32f from location 0 at Tpad, the reference's own walk
+    // (viterbiDecoderButterflyk1.c:200-256)
     uint32_t fin = loc;
     bool fixed = known || (dbg & 4);
-    for (int round = 0; round < 33; round++) {
+    const int rounds = (dbg & kDbgTbCap) ? 1 : 33;
+    uint64_t unproven = 0;
+    for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
         const bool ok = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
+        if (round == rounds) {
+            unproven = bad;
+            break;
+        }
         const uint32_t badf = uint32_t(bad >> (32 * f));
         const bool succ_proven = (uint64_t(badf) >> (blk + 1)) == 0;
         if (!ok && succ_proven) {
@@ -904,6 +856,11 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             fin = loc;
             fixed = true;
         }
+    }
+    if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) {
+        note_guard(hits);
+        uint32_t l = 0;
+        for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48) put_bits48(ob, tlo, tb48(cb0 + kColBytes * (tlo >> 4), l));
     }
     __syncthreads();
 
@@ -1053,13 +1010,22 @@ __global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__
             }
         }
     }
+    // one chain of up to 64 blocks (at most 63 re-walk rounds), with the completeness guard:
+    // unproven after the cap (VTB_DEBUG bit 17: one round), lane 0 walks the frame serially
+    // from location 0 at Tpad
     uint32_t fin = loc;
     bool fixed = known || !active;
-    for (int round = 0; round < 65; round++) {
+    const int rounds = (dbg & kDbgTbCap) ? 1 : 65;
+    bool unproven = false;
+    for (int round = 0;; round++) {
         const uint32_t sfin = __shfl_down(fin, 1);
         const bool okb = fixed || loc_top == sfin;
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
+        if (round == rounds) {
+            unproven = true;
+            break;
+        }
         if (!okb && (bad >> (lane + 1)) == 0) {
             loc = sfin;
             for (int g = kTbWarm / 48; g < nbody; g++) {
@@ -1069,6 +1035,11 @@ __global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__
             fin = loc;
             fixed = true;
         }
+    }
+    if (unproven && lane == 0) {
+        note_guard(table.guard_hits);
+        uint32_t l = 0;
+        for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48) put_bits48(ob, tlo, tb48(col_at(tlo), l));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1095,15 +1066,15 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     column_offsets<NB>(table, off, threadIdx.x);
     if constexpr (STREAM) {
         k9_pair<SOFT, true>(in, in_stride, out, out_stride, T, L, 0, T, Tpad, 0, frames, dbg, ws, ws_wave, blockIdx.x,
-                            blockIdx.x, off, sa);
+                            blockIdx.x, off, sa, nullptr, nullptr, table.guard_hits);
     } else if constexpr (!LOOP) {
         k9_pair<SOFT, false, false, NB>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws,
-                                        ws_wave, blockIdx.x, blockIdx.x, off);
+                                        ws_wave, blockIdx.x, blockIdx.x, off, StreamArgs(), nullptr, nullptr, table.guard_hits);
     } else {
         const size_t pairs = (frames + 1) / 2;
         for (size_t wp = blockIdx.x; wp < pairs; wp += gridDim.x) {
             k9_pair<SOFT, false, false, NB>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, frames, dbg, ws,
-                                            ws_wave, wp, blockIdx.x, off);
+                                            ws_wave, wp, blockIdx.x, off, StreamArgs(), nullptr, nullptr, table.guard_hits);
             __syncthreads();  // LDS (decoded bytes) before the next pair's table ring
         }
     }
@@ -1116,7 +1087,7 @@ size_t grid_waves(const Launch& a, int Tq, int NB = 2) {
     size_t grid = pairs;
     auto kern = NB == 3 ? k9_kernel<false, true, false, 3> : a.soft ? k9_kernel<true, true> : k9_kernel<false, true>;
     const int per_cu =
-        (debug_flags() & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq, NB));
+        (a.dbg & 32) ? 0 : resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0(Tq, NB));
     if (per_cu > 0) {
         const size_t resident = size_t(per_cu) * size_t(a.cus > 0 ? a.cus : 1);
         if (resident < grid) grid = resident;
@@ -1185,8 +1156,7 @@ hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t
     // all working workgroups on one XCD (workgroups go round-robin over the 8 XCDs): the
     // arrival fences and the traceback's word reads stay within one L2 (72.7 against 67.4
     // Mbit/s for speedDecode K=9); $VTB_SEG9_XCD=0 spreads them (measurement)
-    g.xcd = 8;
-    if (const char* v = std::getenv("VTB_SEG9_XCD")) g.xcd = std::atoi(v) > 0 ? 8 : 1;
+    g.xcd = a.seg9_xcd == 0 ? 1 : 8;
     uint8_t* base = static_cast<uint8_t*>(a.ws);
     g.counter = reinterpret_cast<uint32_t*>(base);
     g.met = reinterpret_cast<uint32_t*>(base + 256);
@@ -1195,7 +1165,7 @@ hipError_t launch_k9_seg(const Launch& a, int waves, int wgs, int warm, uint32_t
     auto kern = a.soft ? k9_seg_kernel<true> : k9_seg_kernel<false>;
     note_kernel("k9_seg");
     hipLaunchKernelGGL(kern, dim3(unsigned(nwg * g.xcd)), dim3(64 * waves), lds, a.stream, a.in, a.out, a.T, a.L, delta, Tq,
-                       debug_flags(), a, words, ws_wave, g);
+                       a.dbg, a, words, ws_wave, g);
     return hipGetLastError();
 }
 
@@ -1218,7 +1188,7 @@ hipError_t launch_k9_stream(const Launch& a, const StreamArgs& s) {
     const size_t waves = (a.frames + 1) / 2;
     note_kernel("k9_stream");
     hipLaunchKernelGGL(kern, dim3(unsigned(waves)), dim3(64), (size_t)kRingBytes, a.stream, a.in, a.in_stride, a.out,
-                       a.out_stride, a.T, a.L, 0, a.T, s.t_end, 0, a.frames, 0, a, static_cast<uint8_t*>(a.ws),
+                       a.out_stride, a.T, a.L, 0, a.T, s.t_end, 0, a.frames, a.dbg, a, static_cast<uint8_t*>(a.ws),
                        size_t(kColBytes) / 16 * size_t(s.ring), s);
     return hipGetLastError();
 }
@@ -1247,7 +1217,7 @@ hipError_t launch_k9_n3(const Launch& a) {
     }
     note_kernel(lp ? "k9_n3_loop" : "k9_n3");
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
-                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
+                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, a.dbg, a,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq), StreamArgs());
     return hipGetLastError();
 }
@@ -1267,7 +1237,7 @@ hipError_t launch_k9(const Launch& a) {
     }
     note_kernel(grid < (a.frames + 1) / 2 ? "k9_loop" : "k9");
     hipLaunchKernelGGL(kern, dim3(unsigned(grid)), dim3(64), lds, a.stream, a.in, a.in_stride, a.out,
-                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, debug_flags(), a,
+                       a.out_stride, a.T, a.L, delta, Tq, t_pad(Tq), tb_block(Tq), a.frames, a.dbg, a,
                        static_cast<uint8_t*>(a.ws), ws_wave_bytes(Tq), StreamArgs());
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -162,11 +162,20 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     unsigned fin = st;
     bool fixed = !active || start == T;
     const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
-    for (int round = 0; round <= G; round++) {
+    // (chains of G blocks: at most G - 1 re-walk rounds.)  Completeness guard: a frame with a
+    // block still unproven after the cap (VTB_DEBUG bit 17: one round) is emitted by its lane 0
+    // alone, walking serially from state 0 at T (the reference's walk, :200-256)
+    const int rounds = (table.dbg & kDbgTbCap) ? 1 : G + 1;
+    uint64_t unproven = 0;
+    for (int round = 0;; round++) {
         const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
         const bool ok = fixed || s_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
+        if (round == rounds) {
+            unproven = bad;
+            break;
+        }
         const uint64_t badf = (bad & fmask) >> (fi * G);  // this frame's failed blocks
         if (!ok && (badf >> (lam + 1)) == 0) {
             st = s_top = sf;
@@ -175,11 +184,17 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
             fixed = true;
         }
     }
-    if (!valid || !active) return;
+    int elo = lo, etop = top;  // emitted steps [elo, etop), from s_top after step etop - 1
+    bool emit = active;
+    if (unproven & fmask) {
+        emit = lam == 0, elo = 0, etop = T, s_top = 0;
+        if (lam == 0 && valid) note_guard(table.guard_hits);
+    }
+    if (!valid || !emit) return;
     uint8_t* o = out + myframe * out_stride;
     unsigned byte = 0;
     st = s_top;
-    for (int t = top - 1; t >= lo; t--) {
+    for (int t = etop - 1; t >= elo; t--) {
         byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
         if ((t & 7) == 0 && t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
         st = pred(st, t);

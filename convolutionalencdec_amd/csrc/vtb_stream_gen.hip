@@ -193,11 +193,20 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         for (int t = top - 1; active && t >= lo; t--) s = pred(s, t);
         unsigned fin = s;
         bool fixed = !active || start == hi;
-        for (int round = 0; round <= G; round++) {
+        // (chains of G blocks: at most G - 1 re-walk rounds.)  Completeness guard: a stream with
+        // a block still unproven after the cap (VTB_DEBUG bit 17: one round) is emitted by its
+        // lane 0 alone, walking serially from its known state at hi
+        const int rounds = (table.dbg & kDbgTbCap) ? 1 : G + 1;
+        uint64_t unproven = 0;
+        for (int round = 0;; round++) {
             const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
             const bool ok = fixed || s_top == sf;
             const uint64_t bad = ~__ballot(ok);
             if (bad == 0) break;
+            if (round == rounds) {
+                unproven = bad;
+                break;
+            }
             const uint64_t badf = (bad & fmask) >> (fi * G);  // this stream's failed blocks
             if (!ok && (badf >> (lam + 1)) == 0) {
                 s = s_top = sf;
@@ -206,11 +215,17 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
                 fixed = true;
             }
         }
-        if (active) {
+        int elo = lo, etop = top;  // emitted steps [elo, etop), from s_top after step etop - 1
+        bool emit = active;
+        if (emits && (unproven & fmask)) {
+            emit = lam == 0, elo = e0, etop = hi, s_top = kloc;
+            if (lam == 0) note_guard(table.guard_hits);
+        }
+        if (emit) {
             uint8_t* o = out + myf * out_stride;
             unsigned byte = 0;
             s = s_top;
-            for (int t = top - 1; t >= lo; t--) {
+            for (int t = etop - 1; t >= elo; t--) {
                 byte = ((byte >> 1) | ((s & 1u) << 7)) & 0xffu;
                 const int rel = t - e0;
                 if ((rel & 7) == 0 && t < emit_end) {

@@ -184,3 +184,26 @@ def check(rc, what):
     if rc < 0:
         raise VtbError(rc, what)
     return rc
+
+
+def set_guard_counter(ptr):
+    """Testing: device address of a uint32 that every traceback completeness guard firing in
+    later launches adds 1 to (vtb_debug_set_guard_counter); 0 / None turns it off."""
+    f = lib().vtb_debug_set_guard_counter
+    f.restype, f.argtypes = None, [ctypes.c_void_p]
+    f(ctypes.c_void_p(ptr or 0))
+
+
+def effective_debug_flags():
+    """Testing: the $VTB_DEBUG bits a plan created now carries (the shipped library drops the
+    output-corrupting bits 0-4; vtb_debug_effective_flags)."""
+    f = lib().vtb_debug_effective_flags
+    f.restype, f.argtypes = ctypes.c_int, []
+    return int(f())
+
+
+def measure_build():
+    """True for a -DVTB_MEASURE library (tools/build_variants.sh), which honours them."""
+    f = lib().vtb_debug_measure_build
+    f.restype, f.argtypes = ctypes.c_int, []
+    return bool(f())

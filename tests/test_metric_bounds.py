@@ -27,7 +27,7 @@ U16 = 1 << 16
 
 
 def shipped_period():
-    m = re.search(r"#define VTB_EXP_RN (\d+)", open(SRC).read())
+    m = re.search(r"constexpr int kRenormSoft = (\d+);", open(SRC).read())
     assert m, "soft renormalisation period not found"
     return int(m.group(1))
 
@@ -120,5 +120,5 @@ def test_k7_constants_match_model():
     assert "constexpr uint32_t INIT = 6 * NB * Q + 1;" in src
     assert "static constexpr uint32_t BIAS = SC * (SOFT ? 3060 : 6 * NB);" in src
     assert "constexpr uint32_t PADW = H::SC * INIT * kR1;" in src
-    assert "#define VTB_RENORM_READ(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 2 : (I) == 40)" in src
-    assert "#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % VTB_EXP_RN) == VTB_EXP_RN - 1 : (I) == 47)" in src
+    assert "#define VTB_RENORM_READ(I) (SOFT ? ((I) % kRenormSoft) == kRenormSoft - 2 : (I) == 40)" in src
+    assert "#define VTB_RENORM_APPLY(I) (SOFT ? ((I) % kRenormSoft) == kRenormSoft - 1 : (I) == 47)" in src

@@ -1,15 +1,19 @@
-"""CPU: a model of the block-parallel traceback's verification loop (vtb_k7_lds.hip, k7_pair
-"traceback: verified block-parallel chains") and its round bound.
+"""CPU: a model of the block-parallel traceback's verification loop and its completeness guard
+(DESIGN.md 4.1 "Traceback", 4.2b), checked against the round cap of every loop in the kernels.
 
-Each lane walks one block of a chain from an unverified start; a block is proven when it
-entered on its successor's exit and every later block is proven.  Every round re-walks the
-failed blocks whose successors are all proven, so at least the last unproven block becomes
-proven per round.  A chain of n blocks therefore needs at most n rounds plus the round that
-sees no failure.  Round 3 capped the loop at 33 rounds for every chain, but the split pass
-chains frame A's nA <= 32 blocks and frame B's blocks 2..31 (up to 62): with blocks that keep
-failing (pure-noise frames whose paths do not merge within the walk warm-up) the first
-blocks of frame A left the loop unverified (fuzz case 1366).  The kernel now allows 65
-rounds for split chains (the `rounds` bound); this model pins that arithmetic.
+Each lane walks one block of a chain from an unverified start; a block is proven when it entered
+on its successor's exit and every later block is proven (the chain's last block is known).  A
+round checks every block, then re-walks each failed block whose successors are all proven from
+its successor's exit, so the proven suffix grows by at least one block per round: a chain of n
+blocks needs at most n - 1 re-walk rounds.  Round 3 capped the split pass's loop at 33 rounds
+although its chain has up to 63 blocks, and shipped wrong bits (fuzz case 1366).  Since round 5
+every loop is
+
+    for (round = 0;; round++) { check; if all proven: break; if round == cap: guard; re-walk }
+
+and the guard sends a chain still unproven after `cap` re-walk rounds to the exact slow path
+(tests/test_gpu_tb_guard.py).  This file models that loop and checks each kernel's cap against
+the longest chain its geometry allows.
 """
 import os
 import re
@@ -17,73 +21,102 @@ import re
 import numpy as np
 import pytest
 
-KERNEL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                      "convolutionalencdec_amd", "csrc", "vtb_k7_lds.hip")
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "convolutionalencdec_amd", "csrc")
 
 
-def verify_rounds(entry_top, walk, start_exit, max_rounds):
-    """Run the kernel's verification rounds over one chain (block i's successor is i + 1; the
-    last block is known).  entry_top[i]: the location block i's first walk reached at its top;
-    walk(i, loc): block i's exit when walked from loc; start_exit[i]: its exit from the first
-    walk.  Returns (rounds used, all proven)."""
+def verify(entry_top, walk, start_exit, cap):
+    """The kernel loop over one chain (block i's successor is i + 1; the last block is known).
+    entry_top[i]: the location block i's first walk reached at its top; walk(i, loc): block i's
+    exit walked from loc; start_exit[i]: its exit from the first walk.
+    Returns (re-walk rounds used, proven, guard fired)."""
     n = len(entry_top)
     fin = list(start_exit)
     fixed = [False] * (n - 1) + [True]
-    for rnd in range(max_rounds):
+    rnd = 0
+    while True:
         ok = [fixed[i] or (entry_top[i] == fin[i + 1]) for i in range(n - 1)] + [True]
         bad = [not o for o in ok]
         if not any(bad):
-            return rnd + 1, True
-        # the kernel's lanes act at once, on this round's state
+            return rnd, True, False
+        if rnd == cap:
+            return rnd, False, True
         succ_proven = [not any(bad[i + 1:]) for i in range(n)]
         new_fin = list(fin)
-        for i in range(n - 1):
+        for i in range(n - 1):  # the lanes act at once, on this round's state
             if bad[i] and succ_proven[i]:
                 new_fin[i] = walk(i, fin[i + 1])
                 fixed[i] = True
         fin = new_fin
-    ok = [fixed[i] or (entry_top[i] == fin[i + 1]) for i in range(n - 1)] + [True]
-    return max_rounds, all(ok)
+        rnd += 1
 
 
 def adversarial_chain(n, seed=0):
     """Every block's first walk is wrong (its top location is never its successor's exit)."""
     rng = np.random.default_rng(seed)
-    exits = rng.integers(0, 64, n)
     table = rng.integers(0, 64, (n, 64))
-    start_exit = [int(x) for x in exits]
-    # entry_top never matches any exit a successor can produce: use 64 (no such location)
-    entry_top = [64] * n
-    return entry_top, (lambda i, loc: int(table[i, loc])), start_exit
+    start_exit = [int(x) for x in rng.integers(0, 64, n)]
+    return [64] * n, (lambda i, loc: int(table[i, loc])), start_exit
 
 
-@pytest.mark.parametrize("n", [32, 33, 62, 63])
-def test_rounds_needed_is_chain_length(n):
+@pytest.mark.parametrize("n", [2, 32, 33, 62, 63, 64])
+def test_rewalk_rounds_needed(n):
     top, walk, ex = adversarial_chain(n)
-    used, proven = verify_rounds(top, walk, ex, 10 * n)
-    assert proven and used == n  # n - 1 unproven blocks, one per round, plus the clean round
+    assert verify(top, walk, ex, 10 * n) == (n - 1, True, False)
+    assert verify(top, walk, ex, n - 1)[1]            # a cap of n - 1 suffices
+    if n > 2:
+        assert verify(top, walk, ex, n - 2)[2]        # one less fires the guard
 
 
-def test_split_chain_exceeds_round3_bound():
-    """62-block split chains: 33 rounds leave the first blocks unproven; 65 do not."""
+def test_round3_split_bound_fires_guard():
+    """The round-3 cap (33) on a 62-block split chain now fires the guard instead of shipping
+    the first blocks unverified; the shipped cap (65) proves it."""
     top, walk, ex = adversarial_chain(62, seed=1)
-    assert verify_rounds(top, walk, ex, 33) == (33, False)
-    used, proven = verify_rounds(top, walk, ex, 65)
-    assert proven and used <= 65
+    assert verify(top, walk, ex, 33) == (33, False, True)
+    assert verify(top, walk, ex, 65)[:2] == (61, True)
 
 
-def test_unsplit_chain_fits_33():
-    top, walk, ex = adversarial_chain(32, seed=2)
-    assert verify_rounds(top, walk, ex, 33)[1]
+def test_cap_one_fires_on_long_chains():
+    """VTB_DEBUG bit 17 (cap 1): every chain of 3+ blocks whose first walks all fail."""
+    for n in (3, 32, 64):
+        top, walk, ex = adversarial_chain(n, seed=n)
+        assert verify(top, walk, ex, 1) == (1, False, True)
 
 
-def test_kernel_round_bounds():
-    """The shipped kernel allows 65 rounds on split chains (up to 62 blocks: frame A's nA <= 32
-    and frame B's blocks kB0..63 with kB0 >= 33) and 33 on unsplit ones (32 blocks)."""
-    src = open(KERNEL).read()
-    m = re.search(r"const int rounds = \(SPLIT && sp\) \? (\d+) : (\d+);", src)
-    assert m, "verification round bound not found in vtb_k7_lds.hip"
-    split_rounds, frame_rounds = int(m.group(1)), int(m.group(2))
-    longest_split_chain = 32 + (64 - 33)  # nA <= 32 blocks, frame B's lanes kB0 = 32 + warm/48 >= 33 .. 63
-    assert split_rounds >= longest_split_chain + 1
-    assert frame_rounds >= 32 + 1
+def _caps(fname):
+    src = open(os.path.join(CSRC, fname)).read()
+    caps = re.findall(r"const int rounds = \((?:table\.|a\.)?dbg & kDbgTbCap\) \? 1 : ([^;]+);", src)
+    loops = len(re.findall(r"for \(int round = 0;; round\+\+\)", src))
+    assert len(caps) == loops, (fname, caps, loops)
+    assert not re.search(r"for \(int round = 0; round <", src), f"{fname}: an unguarded verification loop"
+    assert len(re.findall(r"if \(round == rounds\)", src)) == loops, fname
+    return caps
+
+
+def test_every_loop_cap_covers_its_chain():
+    """Each loop's cap against the longest chain its geometry allows (n - 1 re-walks)."""
+    k7 = _caps("vtb_k7_lds.hip")
+    # k7_pair: unsplit frames chain their 32 blocks; the split pass chains frame A's nA <= 32
+    # blocks (t1 <= 32 * 48, split_loop_params / k7_launch) and frame B's lanes kB0..63 with
+    # kB0 = 32 + warm / 48 >= 33 (warm >= 48): nA + 64 - kB0 <= 63 blocks.
+    # (source order: stream_traceback, k7_pair, k7_seg_kernel)
+    assert k7 == ["33", "(SPLIT && sp) ? 65 : 33", "65"]
+    assert 65 >= 63 - 1 and 33 >= 32 - 1
+    src = open(os.path.join(CSRC, "vtb_k7_lds.hip")).read()
+    assert "const int kB0 = 32 + warm / kChunk;" in src
+    assert "if (t1 > 32 * kChunk) return false;" in src and "warm >= kChunk" in src
+    # stream_traceback: 32 blocks per frame; k7_seg_kernel: one chain over the 64 lanes
+    k9 = _caps("vtb_k9.hip")
+    assert k9 == ["33", "33", "65"]  # stream (32 blocks), frame pair (32 per frame), SEG (64)
+    assert _caps("vtb_genk.hip") == ["65"]  # one chain over the 64 lanes
+    assert _caps("vtb_lds_path.hip") == ["G + 1"]  # G lanes (blocks) per frame
+    assert _caps("vtb_stream_gen.hip") == ["G + 1"]
+
+
+@pytest.mark.parametrize("fname", ["vtb_k7_lds.hip", "vtb_k9.hip", "vtb_genk.hip", "vtb_lds_path.hip",
+                                   "vtb_stream_gen.hip"])
+def test_every_guard_has_a_slow_path(fname):
+    """After each loop an unproven chain reaches an exact slow path, and the testing counter
+    notes it (note_guard)."""
+    src = open(os.path.join(CSRC, fname)).read()
+    loops = len(re.findall(r"for \(int round = 0;; round\+\+\)", src))
+    assert len(re.findall(r"note_guard\(", src)) >= loops
