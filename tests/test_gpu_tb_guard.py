@@ -77,12 +77,12 @@ def _set_env(monkeypatch, dbg, kernel):
         monkeypatch.delenv("VTB_KERNEL", raising=False)
 
 
-def _check(counter, got, want, capped, what):
+def _check(counter, got, want, capped, what, reachable=True):
     torch.cuda.synchronize()
     hits = int(counter.item())
     bad = np.flatnonzero((np.asarray(got) != np.asarray(want)).reshape(len(want), -1).any(axis=1))
     assert bad.size == 0, f"{what}: {bad.size} frames differ from the oracle (first {bad[:5].tolist()}), guard hits {hits}"
-    if capped:
+    if capped and reachable:
         assert hits > 0, f"{what}: the capped verification never left a chain unproven (test does not exercise the guard)"
     else:
         assert hits == 0, f"{what}: the guard fired {hits} times at the shipped round caps (a cap is too small)"
@@ -92,17 +92,17 @@ def _check(counter, got, want, capped, what):
 FRAME_CASES = [
     ("k7_lds_soft", 7, 1024, 64, True, NO_SPLIT, None, "k7_lds"),
     ("k7_lds_hard", 7, 1000, 63, False, NO_SPLIT, None, "k7_lds"),
-    ("k7_lds_loop", 7, 128, 20000, False, 0, None, "k7_lds_loop"),
+    ("k7_lds_loop", 7, 512, 8192, False, 0, None, "k7_lds_loop"),
     ("k7_lds_split_soft", 7, 1024, 9, True, 0, None, "k7_lds_split"),
     ("k7_lds_split_hard", 7, 2900, 5, False, 0, None, "k7_lds_split"),
     ("k7_split_loop_soft", 7, 2048, 65, True, 0, "k7s", "k7_split_loop"),
     ("k7_split_loop_hard", 7, 2000, 64, False, 0, "k7s", "k7_split_loop"),
     ("k7_global_soft", 7, 1024, 64, True, 0, "gws", "k7_global"),
     ("k7_global_hard_hybrid", 7, 1024, 64, False, 0, "gws", "k7_global"),
-    ("k7_global_loop", 7, 128, 20000, True, 0, "gws", "k7_global_loop"),
+    ("k7_global_loop", 7, 512, 8192, True, 0, "gws", "k7_global_loop"),
     ("k9_soft", 9, 1024, 64, True, 0, None, "k9"),
     ("k9_hard", 9, 1001, 33, False, 0, None, "k9"),
-    ("k9_loop", 9, 128, 20000, False, 0, None, "k9_loop"),
+    ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
     ("lds_path_k5", 5, 512, 64, False, 0, None, "lds_path"),
     ("lds_path_k7_soft", 7, 700, 16, True, 0, "lds", "lds_path"),
 ]
@@ -150,7 +150,7 @@ def test_single_frame_seg(orc, counter, monkeypatch, K, L, soft, capped):
 
 @pytest.mark.parametrize("capped", [True, False], ids=["cap1", "shipped"])
 @pytest.mark.parametrize("K,soft,gen", [(7, True, False), (7, False, False), (9, True, False), (9, False, False),
-                                        (5, False, True), (7, True, True)])
+                                        (5, False, True), (7, True, True), (9, False, True)])
 def test_streams(orc, counter, monkeypatch, K, soft, gen, capped):
     """vtb_stream_decode (K = 7 / K = 9 stream kernels, the generic stream kernel): a frame in
     three calls, the last one emitting the unmerged remainder in verified chains."""
@@ -171,17 +171,19 @@ def test_streams(orc, counter, monkeypatch, K, soft, gen, capped):
             if nb[f]:
                 got[f].append(np.unpackbits(out[f])[:nb[f]])
     got = np.stack([np.concatenate(g) for g in got])
-    _check(counter, got, want, capped, f"stream K={K} soft={soft} gen={gen}")
+    # (K = 5: 16-state survivor paths merge within the 80-step walk warm-up even on pure noise,
+    # so one re-walk round always suffices there; the generic kernel's guard is reached at K = 7, 9)
+    _check(counter, got, want, capped, f"stream K={K} soft={soft} gen={gen}", reachable=K != 5)
 
 
 @pytest.mark.parametrize("capped", [True, False], ids=["cap1", "shipped"])
-@pytest.mark.parametrize("which", ["genk_k2", "genk_k3", "k7_lds_n3", "k9_n3"])
+@pytest.mark.parametrize("which", ["genk_k2", "genk_k2_K5", "k7_lds_n3", "k9_n3"])
 def test_general_k(orc, counter, monkeypatch, which, capped):
     """vtb_genk_decode_device: the general-k kernel (one chain of up to 64 blocks over the
     frame's boundaries) and the rate-1/3 K=7 / K=9 fast kernels."""
     _set_env(monkeypatch, CAP if capped else 0, None)
     if which.startswith("genk"):
-        k, K, g = GENK_CODES[0] if which == "genk_k2" else GENK_CODES[1]
+        k, K, g = GENK_CODES[0] if which == "genk_k2" else GENK_CODES[3]  # 64 / 256 states
         L, F = 1536, 12
         _, a = genk_frames(orc, k, K, g, L, F // 2, 0.5, 31)
         _, b = genk_frames(orc, k, K, g, L, F - F // 2, 0.05, 32)

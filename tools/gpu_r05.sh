@@ -14,7 +14,7 @@ PYT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-metho
 for step in "$@"; do
   case $step in
     guard)
-      timeout -k 10 600 $PYT tests/test_gpu_tb_guard.py -m gpu > $O/guard.log 2>&1 || { tail -40 $O/guard.log; exit 1; }
+      timeout -k 10 600 ${PYT/-x /} tests/test_gpu_tb_guard.py -m gpu > $O/guard.log 2>&1 || { tail -40 $O/guard.log; exit 1; }
       tail -2 $O/guard.log ;;
     suite)
       timeout -k 10 900 $PYT tests/ -m gpu > $O/gpu_tests_full.log 2>&1 || { tail -40 $O/gpu_tests_full.log; exit 1; }
