@@ -334,13 +334,90 @@ def load_kernel_time(workload_key):
     return ent if ent is not None and isinstance(ent.get("avg_ns"), (int, float)) else None
 
 
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 integer VALU instruction per 4 cycles per
-# SIMD (v_add_u32 / v_pk_min_u16 / DPP adds: tools/probes/isa_bench.hip, profiles/r01), at the
-# 2.4 GHz peak engine clock.
-VALU_PEAK_G = 256 * 4 * 2.4 / 4
-# The SIMD-32's full-rate issue (a wave64 instruction every 2 cycles, MI355X_MICROARCH.md:54),
-# reached only by the plain 32-bit ops with two or more waves per SIMD (profiles/r01/isa_bench*.txt)
+# VALU issue peaks.  The SIMD-32's full rate, a wave64 instruction every 2 cycles
+# (MI355X_MICROARCH.md:54), at the 2.4 GHz peak engine clock over 256 CUs x 4 SIMDs: the
+# absolute peak `roofline.secondary` reports against.  The 4-cycle rate is what the integer ops
+# this path depends on (v_pk_min_u16, DPP adds) issue at; only plain 32-bit ops reach the 2-cycle
+# rate, with two or more waves per SIMD (profiles/r01/isa_bench*.txt).  The mix of each kernel's
+# ACS loop prices between the two (`issue_priced`, tools/isa_mix.py, profiles/isa_mix.json).
 VALU_PEAK_2CYC_G = 256 * 4 * 2.4 / 2
+VALU_PEAK_4CYC_G = 256 * 4 * 2.4 / 4
+
+# roofline.secondary.note per kernel instance (vtb_debug_last_kernel)
+KERNEL_NOTES = {
+    "k7_lds": "K=7 pair kernel (vtb_k7_lds.hip): packed u16 ACS, 2 frames per wave64, survivors in LDS, one wave "
+              "per frame pair",
+    "k7_lds_loop": "K=7 pair kernel, persistent over frame pairs: packed u16 ACS, 2 frames per wave64, survivors in "
+                   "LDS",
+    "k7_lds_split": "K=7 split frames: one frame per wave64 as two halves in the u16 halves, survivors in LDS",
+    "k7_split_loop": "K=7 persistent split kernel: one frame per wave64 as two halves, survivors in LDS, in-wave "
+                     "fix-up, unconverged frames to the list kernel",
+    "k7_global": "K=7 pair kernel with survivor words in a global workspace (newest steps in LDS for hard input)",
+    "k7_global_loop": "K=7 pair kernel, persistent, survivor words in a global workspace",
+    "k9": "K=9 frame kernel (vtb_k9.hip): 4 metric registers per lane, 2 frames per wave64, survivor words in a "
+          "global workspace",
+    "k9_loop": "K=9 frame kernel, persistent over frame pairs, survivor words in a global workspace",
+    "lds_path": "generic K=3..9 LDS kernel (vtb_lds_path.hip): int32 metrics, partners by ds_bpermute",
+}
+
+
+def load_isa_mix(kernel, soft):
+    """The issue-priced VALU bound of `kernel`'s ACS loop on this library (profiles/isa_mix.json,
+    tools/isa_mix.py), or None."""
+    return _stamped("isa_mix.json", f"{kernel}/{'soft' if soft else 'hard'}")
+
+
+def roofline_block(alg_bytes, avg_ms, n_avg, kern_ms, launch_ms, issue_us, state_steps, kernel, traffic=None,
+                   kernel_time=None, valu=None, mix=None):
+    """The bench line's `roofline` object.  HBM roofline of the decode kernel: algorithmic bytes
+    per launch / the average launch time avg_ms (back-to-back launches) against
+    8 TB/s, `traffic` = PMC-measured HBM bytes per launch.  `secondary`: the bound that holds,
+    integer VALU issue, against the 2-cycle peak and the kernel's issue-priced mix."""
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    sec = {"bound": "valu", "kernel": kernel,
+           "note": KERNEL_NOTES.get(kernel, "see DESIGN.md 5") + "; DESIGN.md 5",
+           "state_steps_per_s": round(state_steps / (avg_ms * 1e-3))}
+    ach = None
+    if valu:
+        ach = valu["valu_wave_insts_per_launch"] / (avg_ms * 1e-3) / 1e9
+        sec.update({"achieved": round(ach, 2), "unit": "G wave64-VALU-instr/s",
+                    "peak": VALU_PEAK_2CYC_G, "frac": round(ach / VALU_PEAK_2CYC_G, 4),
+                    "peak_note": "2-cycle wave64 issue (MI355X_MICROARCH.md:54), 1,024 SIMDs at 2.4 GHz",
+                    "peak_4cycle": VALU_PEAK_4CYC_G, "frac_4cycle": round(ach / VALU_PEAK_4CYC_G, 4),
+                    "valu_wave_insts_per_launch": valu["valu_wave_insts_per_launch"]})
+    if mix:
+        ip = {"peak": mix["priced_peak_G"], "valu_per_wave_step": mix["valu_per_wave_step"],
+              "priced_cycles_per_wave_step": mix["priced_cycles_per_wave_step"],
+              "note": "the ACS loop's own instruction mix priced at the measured issue costs (2.8 / 4.6 / 9.4 "
+                      "cycles: plain / packed, DPP, VOP3 / permlane swap; tools/isa_mix.py); the launch also "
+                      "holds the traceback"}
+        if ach is not None:
+            ip["frac"] = round(ach / mix["priced_peak_G"], 4)
+        sec["issue_priced"] = ip
+    issue_bound = issue_us is not None and issue_us * 1e-3 >= 0.8 * avg_ms
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 3),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6),
+        "traffic": traffic,
+        "kernel_avg_ms": round(avg_ms, 5),
+        "kernel_avg_note": f"HIP events around {n_avg} back-to-back launches on the launch stream, opened behind a "
+                           "running launch (no first-launch latency); achieved/frac use it",
+        "kernel_avg_issue_bound": issue_bound,
+        "rocprof_avg_ms": round(kernel_time["avg_ns"] * 1e-6, 5) if kernel_time else None,
+        "timed_span_ms": round(kern_ms, 5),
+        "timed_span_note": "event span of the timed region / steps; opens on an idle stream, so it includes the "
+                           "first launch's dispatch latency",
+        "per_launch_pass_ms": {"min": round(min(launch_ms), 5), "median": round(float(np.median(launch_ms)), 5),
+                               "max": round(max(launch_ms), 5), "first": round(launch_ms[0], 5),
+                               "note": "untimed pass after the timed region, an event after every launch"},
+        "host_issue_us_per_launch": round(issue_us, 2) if issue_us is not None else None,
+        "algorithmic_bytes_per_launch": alg_bytes,
+        # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)
+        "secondary": sec,
+    }
 
 
 def stream_bench(args, dev, local, world):
@@ -669,19 +746,14 @@ def main():
     value = total_bits / (elapsed / args.steps) / 1e6
     in_b = (2 if soft else 1) * T
     alg_bytes = F * (in_b + (L + 7) // 8)
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     workload_key = f"K{code[0]}_{'soft' if soft else 'hard'}_F{F}_L{L}"
-    traffic = load_traffic(workload_key)
-    valu = load_valu(workload_key)
-    kt = load_kernel_time(workload_key)
-    secondary = {"bound": "valu", "state_steps_per_s": round(F * (1 << (code[0] - 1)) * T / (avg_ms * 1e-3)),
-                 "note": "packed u16 ACS, 2 frames per wave64; see DESIGN.md 5"}
-    if valu:
-        ach = valu["valu_wave_insts_per_launch"] / (avg_ms * 1e-3) / 1e9
-        secondary.update({"achieved": round(ach, 2), "peak": VALU_PEAK_G, "unit": "G wave64-VALU-instr/s",
-                          "frac": round(ach / VALU_PEAK_G, 4),
-                          "peak_2cycle": VALU_PEAK_2CYC_G, "frac_2cycle": round(ach / VALU_PEAK_2CYC_G, 4),
-                          "valu_wave_insts_per_launch": valu["valu_wave_insts_per_launch"]})
+    from convolutionalencdec_amd import native
+
+    kernel = native.last_kernel()
+    roofline = roofline_block(alg_bytes, avg_ms, n_avg, kern_ms, launch_ms, issue.get("us"),
+                              F * (1 << (code[0] - 1)) * T, kernel, traffic=load_traffic(workload_key),
+                              kernel_time=load_kernel_time(workload_key), valu=load_valu(workload_key),
+                              mix=load_isa_mix(kernel, soft))
 
     if rank != 0:
         if world > 1:
@@ -718,28 +790,7 @@ def main():
             "host_buffers_mbps": host_mbps,
             "decoded_ber": ber,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 3),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6),
-            "traffic": traffic,
-            "kernel_avg_ms": round(avg_ms, 5),
-            "kernel_avg_note": f"HIP events around {n_avg} back-to-back launches on the launch stream, opened "
-                               "behind a running launch (no first-launch latency); achieved/frac use it",
-            "rocprof_avg_ms": round(kt["avg_ns"] * 1e-6, 5) if kt else None,
-            "timed_span_ms": round(kern_ms, 5),
-            "timed_span_note": "event span of the timed region / steps; opens on an idle stream, so it includes "
-                               "the first launch's dispatch latency",
-            "per_launch_pass_ms": {"min": round(min(launch_ms), 5), "median": round(float(np.median(launch_ms)), 5),
-                                   "max": round(max(launch_ms), 5), "first": round(launch_ms[0], 5),
-                                   "note": "untimed pass after the timed region, an event after every launch"},
-            "host_issue_us_per_launch": round(issue["us"], 2) if "us" in issue else None,
-            "algorithmic_bytes_per_launch": alg_bytes,
-            # the path is integer-VALU bound (add-compare-select), not HBM bound: SURVEY.md 8(d)
-            "secondary": secondary,
-        },
+        "roofline": roofline,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

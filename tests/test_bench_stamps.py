@@ -77,12 +77,68 @@ def test_kernel_time_stamp(fake_repo):
     assert bench.load_kernel_time(KEY) is None
 
 
+def _block(**kw):
+    args = dict(alg_bytes=8962048, avg_ms=0.0316, n_avg=50, kern_ms=0.0326, launch_ms=[0.034, 0.0339, 0.0391],
+                issue_us=4.4, state_steps=4096 * 64 * 1030, kernel="k7_lds")
+    args.update(kw)
+    return bench.roofline_block(**args)
+
+
 def test_roofline_fields_named_for_what_they_time():
-    """The roofline block names its kernel time kernel_avg_ms (back-to-back launches, no
-    first-launch latency) and computes achieved from it; the timed region's event span is
-    timed_span_ms (verdict r03 item 5)."""
-    src = open(bench.__file__).read()
-    assert '"kernel_avg_ms": round(avg_ms, 5)' in src
-    assert '"timed_span_ms": round(kern_ms, 5)' in src
-    assert "achieved = alg_bytes / (avg_ms * 1e-3) / 1e9" in src
-    assert '"kernel_ms"' not in src.split("def main")[1]
+    """kernel_avg_ms (back-to-back launches) drives achieved / frac; the timed region's span is
+    timed_span_ms (verdict r03 item 5); the host's issue time sits beside it and flags a
+    kernel_avg_ms that issue could explain."""
+    r = _block()
+    assert r["kernel_avg_ms"] == 0.0316 and r["timed_span_ms"] == 0.0326
+    assert r["achieved"] == pytest.approx(8962048 / 31.6e-6 / 1e9, rel=1e-4)
+    assert r["frac"] == pytest.approx(r["achieved"] / 8000.0, rel=1e-4)
+    assert r["host_issue_us_per_launch"] == 4.4 and r["kernel_avg_issue_bound"] is False
+    assert _block(issue_us=30.0)["kernel_avg_issue_bound"] is True
+    assert r["per_launch_pass_ms"]["max"] == 0.0391 and r["traffic"] is None and r["rocprof_avg_ms"] is None
+    assert _block(kernel_time={"avg_ns": 32030.0})["rocprof_avg_ms"] == 0.03203
+
+
+def test_valu_secondary_against_two_cycle_peak():
+    """roofline.secondary: the 2-cycle wave64 peak (1,228.8 G/s, MI355X_MICROARCH.md) is `peak`,
+    the 4-cycle rate a named field beside it, and the kernel's issue-priced mix (tools/isa_mix.py)
+    its own bound (verdict r04 item 5)."""
+    mix = {"priced_peak_G": 607.9, "valu_per_wave_step": 5.0, "priced_cycles_per_wave_step": 20.212}
+    r = _block(valu={"valu_wave_insts_per_launch": 11270238}, mix=mix)["secondary"]
+    ach = 11270238 / 31.6e-6 / 1e9
+    assert r["achieved"] == pytest.approx(ach, abs=0.01)
+    assert r["peak"] == 1228.8 and r["frac"] == pytest.approx(ach / 1228.8, abs=1e-4)
+    assert r["peak_4cycle"] == 614.4 and r["frac_4cycle"] == pytest.approx(ach / 614.4, abs=1e-4)
+    assert r["issue_priced"]["peak"] == 607.9 and r["issue_priced"]["frac"] == pytest.approx(ach / 607.9, abs=1e-4)
+    assert r["state_steps_per_s"] == round(4096 * 64 * 1030 / 31.6e-6)
+    no = _block()["secondary"]
+    assert "frac" not in no and "issue_priced" not in no
+
+
+@pytest.mark.parametrize("kernel", ["k7_lds", "k7_lds_loop", "k7_split_loop", "k9", "lds_path"])
+def test_secondary_note_per_kernel(kernel):
+    r = _block(kernel=kernel)["secondary"]
+    assert r["kernel"] == kernel and r["note"].startswith(bench.KERNEL_NOTES[kernel])
+    assert len({bench.KERNEL_NOTES[k] for k in bench.KERNEL_NOTES}) == len(bench.KERNEL_NOTES)
+
+
+def test_isa_mix_stamp(fake_repo):
+    root, sha = fake_repo
+    write(root, "isa_mix.json", {"k7_lds/soft": {"priced_peak_G": 607.9, "lib_sha16": sha},
+                                 "k9/hard": {"priced_peak_G": 606.5, "lib_sha16": "0" * 16}})
+    assert bench.load_isa_mix("k7_lds", True)["priced_peak_G"] == 607.9
+    assert bench.load_isa_mix("k7_lds", False) is None
+    assert bench.load_isa_mix("k9", False) is None
+
+
+def test_committed_isa_mix_covers_the_bench_configs():
+    """profiles/isa_mix.json (tools/isa_mix.py) prices the kernels of every BASELINE config line
+    from the 48-step chunk loop: 48 v_pk_min per metric register."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(repo, "profiles", "isa_mix.json")) as fh:
+        mix = json.load(fh)
+    for key, regs in (("k7_lds/soft", 1), ("k7_lds/hard", 1), ("k7_split_loop/soft", 1), ("k7_split_loop/hard", 1),
+                      ("k7_lds_loop/soft", 1), ("k9/hard", 4)):
+        ent = mix[key]
+        assert ent["mix"]["pk_min"] == 48 * regs and ent["loop_steps"] == 48, key
+        assert 500 < ent["priced_peak_G"] < 1228.8, key
+        assert len(ent["lib_sha16"]) == 16

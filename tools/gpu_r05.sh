@@ -3,7 +3,13 @@
 #   tools/gpu_r05.sh guard   the completeness-guard tests (tests/test_gpu_tb_guard.py)
 #   tools/gpu_r05.sh suite   the whole GPU suite, smoke() and the driver's bench command
 #   tools/gpu_r05.sh bench   the driver's bench command only (twice)
-#   tools/gpu_r05.sh prof    rocprofv3 kernel trace + stats of the bench command
+#   tools/gpu_r05.sh prof    rocprofv3 kernel trace + stats of the bench command (the library's
+#                            sha beside it for tools/kernel_time_summary.py)
+#   tools/gpu_r05.sh fuzz    one fuzz sweep and one fix-up sweep on this library (2,000 cases per
+#                            family), plus the fuzz sweep again with every traceback verification
+#                            capped at one round (VTB_DEBUG bit 17: the guards' slow paths)
+#   tools/gpu_r05.sh stamps  PMC passes of every config line, the config lines, SQ passes of the
+#                            headline (summarised on the CPU: tools/traffic_summary.py, ...)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05
@@ -29,9 +35,22 @@ for step in "$@"; do
         cut -c1-300 $O/bench_$i.json
       done ;;
     prof)
-      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      export TMPDIR=/tmp
+      rm -rf $O/prof && mkdir -p $O/prof && echo "$sha" > $O/prof/lib_sha16.txt
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_bench.json 2> $O/prof.err || { tail $O/prof.err; exit 1; }
       find $O/prof -name '*kernel_stats.csv' | head -3 ;;
+    fuzz)
+      mkdir -p $O/fuzz
+      VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5005 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_seed5005.log 2>&1 || { tail -30 $O/fuzz/fuzz_seed5005.log; exit 1; }
+      tail -n 1 $O/fuzz/fuzz_seed5005.log
+      VTB_FIXUP_N=2000 VTB_FIXUP_SEED=5007 timeout -k 10 600 ${PYT/-x /} tests/test_gpu_split_fixup.py -m gpu -k fixup_family > $O/fuzz/fixup_seed5007.log 2>&1 || { tail -30 $O/fuzz/fixup_seed5007.log; exit 1; }
+      tail -n 1 $O/fuzz/fixup_seed5007.log
+      VTB_DEBUG=131072 VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5006 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_cap1_seed5006.log 2>&1 || { tail -30 $O/fuzz/fuzz_cap1_seed5006.log; exit 1; }
+      tail -n 1 $O/fuzz/fuzz_cap1_seed5006.log ;;
+    stamps)
+      timeout -k 10 900 bash tools/pmc_passes.sh head c2 c3s c3h c4 c5 || exit 1
+      timeout -k 10 600 bash tools/configs.sh && cp gpurun_out/configs.jsonl $O/configs.jsonl || exit 1
+      TAG=head timeout -k 10 400 bash tools/pmc_stalls.sh || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round 4: rocprofv3 PMC passes (one counter group per run, kernel trace only, no other tracing) for the
-# workloads named on the command line; summarise afterwards with
-#   python tools/traffic_summary.py gpurun_out/pmc_<wl> r04 <key>
+# rocprofv3 PMC passes (one counter group per run, kernel trace only, no other tracing) for the
+# workloads named on the command line, the library's sha written beside each workload's passes;
+# summarise afterwards with
+#   python tools/traffic_summary.py gpurun_out/pmc_<wl> r05 <key>
 # Workloads (bench.py arguments, workload key):
 #   head   K7 soft 4096 x 1024   (the bench line)      K7_soft_F4096_L1024   fetch write valu
 #   c2     K7 hard 4096 x 1024                          K7_hard_F4096_L1024   fetch write valu
@@ -13,6 +14,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+sha=$(sha256sum convolutionalencdec_amd/lib/libviterbi_amd.so | cut -c1-16)
 for wl in "$@"; do
   passes="fetch write"
   case $wl in
@@ -21,9 +23,10 @@ for wl in "$@"; do
     c3s) args="--frames 65536 --frame-bits 2048 --steps 5 --warmup 1" ; passes="fetch write valu" ;;
     c3h) args="--frames 65536 --frame-bits 2048 --steps 5 --warmup 1 --hard" ; passes="fetch write valu" ;;
     c4) args="--K 9 --hard --steps 20 --warmup 2" ; passes="fetch write valu" ;;
-    c5) args="--frames 131072 --steps 5 --warmup 1" ;;
+    c5) args="--frames 131072 --steps 5 --warmup 1" ; passes="fetch write valu" ;;
     *) echo "unknown workload $wl"; exit 2 ;;
   esac
+  mkdir -p gpurun_out/pmc_$wl && echo "$sha" > gpurun_out/pmc_$wl/lib_sha16.txt
   for pass in $passes; do
     case $pass in
       fetch) ctr="FETCH_SIZE" ;;

@@ -11,7 +11,6 @@ K7_soft_F4096_L1024), the same halving, so the fetch figure is doubled; WRITE_SI
 the output bytes exactly (524,288) and is used as is.
 """
 import csv
-import hashlib
 import json
 import os
 import sys
@@ -20,10 +19,13 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"  # holds pmc_fetch/, p
 rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
 key = sys.argv[3] if len(sys.argv) > 3 else "K7_soft_F4096_L1024"
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# every entry is stamped with the library it was measured on; bench.py reports null for
-# counters of any other binary
-with open(os.path.join(repo, "convolutionalencdec_amd", "lib", "libviterbi_amd.so"), "rb") as _fh:
-    LIB_SHA16 = hashlib.sha256(_fh.read()).hexdigest()[:16]
+# every entry is stamped with the library it was measured on (bench.py reports null for counters
+# of any other binary): the sha the profiling run wrote beside its passes (tools/pmc_passes.sh,
+# <root>/lib_sha16.txt), not the library present when this script runs
+_sha = os.path.join(root, "lib_sha16.txt")
+if not os.path.exists(_sha):
+    raise SystemExit(f"{_sha} missing: the profiled run's library stamp")
+LIB_SHA16 = open(_sha).read().split()[-1].strip()
 
 
 def mean_counter(d, name):
