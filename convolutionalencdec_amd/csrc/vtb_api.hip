@@ -191,7 +191,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     // frame to the list (without the fix-up 1.065 ms, 1,528 frames listed); hard p = 0.056
     // 0.808 ms against 0.805 for the global-survivor variant, whose survivor words leave the CU
     // (7.5x the algorithmic HBM bytes).  VTB_KERNEL=k7s forces it wherever it applies;
-    // VTB_DEBUG bit 12 (measurement only): never.
+    // VTB_DEBUG bit 12 (testing): never.
     const bool want_split = k7s || (any && !k7_in_lds);
     if (want_split && !(a.dbg & 4096) && vtb::k7_split_loop_supported(a)) {
         if (!workspace(vtb::k7_split_loop_workspace_bytes(a))) return VTB_ERR_NOMEM;

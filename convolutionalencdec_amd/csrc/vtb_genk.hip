@@ -39,7 +39,7 @@ struct GenArgs {
     int ptr_bytes;   // survivor-pointer bytes per frame (gen_ptr_bytes)
     int u8;          // VTB_GENK_K1_REFERENCE_U8: the reference's k=1 butterfly arithmetic (below)
     int warm;        // traceback warm-up steps per block (any value is exact: the walk is verified)
-    int dbg;         // $VTB_DEBUG (measurement only): bit 0 skips the traceback, bit 1 the ACS
+    int dbg;         // the knobs' $VTB_DEBUG: bit 17 caps the verification; -DVTB_MEASURE builds: bit 0 skips the traceback, 1 the ACS
     uint32_t* hits;  // testing: completeness-guard counter (Launch::guard_hits), null in production
     uint32_t rg[8];  // generators bit-reversed over k*K bits (convEncode.c:163-174)
 };

@@ -283,7 +283,8 @@ __device__ __forceinline__ uint64_t tb_body_spec(uint32_t cb, uint32_t& l4, uint
     return bits;
 }
 
-// The serial form is the shipped one.  The speculative form (round 1, measurement only) measured slower where it matters: LDS words 6 % per 4,096-frame launch (2.5 random
+// The serial form is the shipped one.  The speculative form (round 1, measurement only)
+// measured slower where it matters: LDS words 6 % per 4,096-frame launch (2.5 random
 // reads per window cost more LDS bandwidth than the latency they hide, with 8 waves per CU
 // tracing back at once), global words 2 % slower on config C3 (65,536 x 2,048 bits: the
 // extra loads queue behind other waves' traffic), 2 % faster only for one 4,096-frame round
@@ -734,7 +735,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     uint8_t* tab = smem;
     uint32_t* dec = reinterpret_cast<uint32_t*>(smem + r0);
     const int lane = SEG ? int(threadIdx.x & 63) : int(threadIdx.x);
-    if (dbg & 16) return;  // measurement only: launch cost
+    if (dbg & 16) return;  // (-DVTB_MEASURE builds only) launch cost
     // SPLIT: one frame per wave, its two halves in the u16 halves of the registers: A = steps
     // [0, t1), B = steps [t1 - 96, T) (96 warm-up steps from equal start metrics).  If B's
     // metrics at t1 equal A's up to a constant, B's decisions from t1 on are the frame's
@@ -1633,7 +1634,7 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
 // bits); soft input reads a word per 2 steps, and a wave walks at the pace of its slowest
 // lane, so the LDS lanes gained nothing while every window paid for both loads: C3 soft
 // 1.16-1.17 vs 1.07 ms (profiles/r02/hybrid_survivors_ab.txt).  VTB_DEBUG bit 11
-// (measurement only): none.
+// (testing): none.
 int gs_lds_steps(const Launch& a) {
     const int T = a.T;
     if (a.soft || (a.dbg & 2048)) return 0;
@@ -1690,7 +1691,7 @@ hipError_t launch_k7(const Launch& a) {
     const char* name = GS ? (loop ? "k7_global_loop" : "k7_global") : (loop ? "k7_lds_loop" : "k7_lds");
     // Batches the CUs hold at one frame per wave (up to 2 per SIMD at L = 1024) run split
     // (one frame per wave, both halves at once: k7_pair SPLIT): twice the waves, about half
-    // the dependent steps per wave.  VTB_DEBUG bit 8 (measurement only): never split.
+    // the dependent steps per wave.  VTB_DEBUG bit 8 (testing): never split.
     if (!GS && a.T >= 240 && split_t1(a.T) <= 32 * kChunk && !(a.dbg & 256)) {
         auto ks = kernel_of<false, false, true>(a);
         const int per_cu = resident_per_cu(reinterpret_cast<const void*>(ks), lds);
