@@ -71,8 +71,9 @@ void set_debug_tstamp(unsigned long long* p);
 //   ring only, 8 never split frames across the halves of a wave, 10 no single-frame SEG kernel,
 //   11 global-survivor variant without its LDS part, 12 never the persistent split kernel,
 //   13 full last chunk, 14 no in-wave split fix-up, 15 fix-up on every split frame, 16 fix-up
-//   checkpoints never match, 17 traceback verification capped at one round (every kernel's
-//   completeness guard then sends each chain not yet proven to its exact slow path).
+//   checkpoints never match, 17 traceback verification allows no re-walk round (every kernel's
+//   completeness guard then sends each chain its first walks did not prove to its exact slow
+//   path).
 // Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
 //   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE
 //   build (tools/build_variants.sh) honours them; the shipped library masks them off.

@@ -75,16 +75,18 @@ def test_round3_split_bound_fires_guard():
     assert verify(top, walk, ex, 65)[:2] == (61, True)
 
 
-def test_cap_one_fires_on_long_chains():
-    """VTB_DEBUG bit 17 (cap 1): every chain of 3+ blocks whose first walks all fail."""
-    for n in (3, 32, 64):
+def test_cap_zero_fires_on_any_failed_first_walk():
+    """VTB_DEBUG bit 17 (cap 0): every chain with a block whose first walk did not verify."""
+    for n in (2, 32, 64):
         top, walk, ex = adversarial_chain(n, seed=n)
-        assert verify(top, walk, ex, 1) == (1, False, True)
+        assert verify(top, walk, ex, 0) == (0, False, True)
+    top, walk, ex = adversarial_chain(8, seed=3)
+    assert verify([walk(i + 1, 0) if i < 7 else 0 for i in range(8)], walk, [walk(i, 0) for i in range(8)], 0)[:2] == (0, True)
 
 
 def _caps(fname):
     src = open(os.path.join(CSRC, fname)).read()
-    caps = re.findall(r"const int rounds = \((?:table\.|a\.)?dbg & kDbgTbCap\) \? 1 : ([^;]+);", src)
+    caps = re.findall(r"const int rounds = \((?:table\.|a\.)?dbg & kDbgTbCap\) \? 0 : ([^;]+);", src)
     loops = len(re.findall(r"for \(int round = 0;; round\+\+\)", src))
     assert len(caps) == loops, (fname, caps, loops)
     assert not re.search(r"for \(int round = 0; round <", src), f"{fname}: an unguarded verification loop"
