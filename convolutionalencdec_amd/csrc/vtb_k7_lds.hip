@@ -1361,7 +1361,7 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             break;
         }
         bool succ_proven;
-        if (SPLIT && sp) {  // one chain: frame A's blocks 0..nA-1, then frame B's blocks 2..31
+        if (SPLIT && sp) {  // one chain: frame A's blocks 0..nA-1, then frame B's blocks kB0-32..31
             const uint64_t cm = (bad & ((uint64_t(1) << nA) - 1)) | ((bad >> kB0) << nA);
             const int pos = f == 0 ? blk : nA + lane - kB0;
             succ_proven = (cm >> (pos + 1)) == 0;
