@@ -376,15 +376,16 @@ __global__ __launch_bounds__(64) void genk_kernel(const uint8_t* __restrict__ in
         int s_top = s;
         for (int i = top - 1; active && i >= lo; i--) s = ptr(i, s);
         // (one chain of up to 64 blocks: at most 63 re-walk rounds.)  Completeness guard: a block
-        // still unproven after the cap (VTB_DEBUG bit 17: no re-walk) sends the frame to its
+        // still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) sends the frame to its
         // serial walk -- lane 0 emits every window from state 0 at the last boundary
         int fin = s;
         bool fixed = !active || start == nb;
-        const int rounds = (a.dbg & kDbgTbCap) ? 0 : 65;
+        const bool tbforce = (a.dbg & kDbgTbCap) != 0;
+        const int rounds = tbforce ? 0 : 65;
         bool unproven = false;
         for (int round = 0;; round++) {
             const int sf = __shfl_down(fin, 1);
-            const bool ok = fixed || s_top == sf;
+            const bool ok = fixed || (s_top == sf && !tbforce);
             const uint64_t bad = ~__ballot(ok);
             if (bad == 0) break;
             if (round == rounds) {

@@ -71,8 +71,8 @@ void set_debug_tstamp(unsigned long long* p);
 //   ring only, 8 never split frames across the halves of a wave, 10 no single-frame SEG kernel,
 //   11 global-survivor variant without its LDS part, 12 never the persistent split kernel,
 //   13 full last chunk, 14 no in-wave split fix-up, 15 fix-up on every split frame, 16 fix-up
-//   checkpoints never match, 17 traceback verification allows no re-walk round (every kernel's
-//   completeness guard then sends each chain its first walks did not prove to its exact slow
+//   checkpoints never match, 17 forced completeness guards (every traceback chain with a block not
+//   known from the frame end skips its checks and re-walks and takes the guard's exact slow
 //   path).
 // Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
 //   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE

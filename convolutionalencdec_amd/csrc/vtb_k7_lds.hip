@@ -573,15 +573,16 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
         }
         // verification, as in the frame decoder (the last active block of a frame is known; a
         // chain of 32 blocks needs at most 31 re-walk rounds), with its completeness guard: a
-        // frame still unproven after the cap (VTB_DEBUG bit 17: no re-walk) is walked serially
+        // frame still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is walked serially
         // from its known location at hi by lane 32f
         uint32_t fin = loc;
         bool fixed = known || !active;
-        const int rounds = (dbg & kDbgTbCap) ? 0 : 33;
+        const bool tbforce = (dbg & kDbgTbCap) != 0;
+        const int rounds = tbforce ? 0 : 33;
         bool unproven = false;
         for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
-            const bool ok = fixed || loc_top == sf;
+            const bool ok = fixed || (loc_top == sf && !tbforce);
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0) break;
@@ -1345,15 +1346,16 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     // block still unproven there never reaches the output -- the split pass sends its frame to
     // the slow path (the unsplit pass, or the list kernel), an unsplit frame is traced back
     // serially from location 0 at Tpad (the reference's own walk, viterbiDecoderButterflyk1.c:
-    // 200-256).  VTB_DEBUG bit 17 allows no re-walk round (cap 0) to exercise both.
+    // 200-256).  VTB_DEBUG bit 17 sends every chain with a walked block there (no check, no re-walk), to exercise both.
     uint32_t fin = loc;  // survivor's location at step blk * tbb
     bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement builds only): skip verification
-    const int rounds = (dbg & kDbgTbCap) ? 0 : (SPLIT && sp) ? 65 : 33;
+    const bool tbforce = (dbg & kDbgTbCap) != 0;
+    const int rounds = tbforce ? 0 : (SPLIT && sp) ? 65 : 33;
     uint64_t unproven = 0;
     for (int round = 0;; round++) {
         // successor's exit (lane 31, frame A's last block, is known)
         const uint32_t sf = (SPLIT && sp) ? __shfl(fin, lane == nA - 1 ? kB0 : (lane + 1) & 63) : __shfl_down(fin, 1);
-        const bool ok = fixed || loc_top == sf;
+        const bool ok = fixed || (loc_top == sf && !tbforce);
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
         if (round == rounds) {
@@ -1579,15 +1581,16 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
         }
     }
     // one chain of up to 64 blocks (at most 63 re-walk rounds), with the completeness guard:
-    // unproven after the cap (VTB_DEBUG bit 17: no re-walk), lane 0 walks the frame serially
+    // unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block), lane 0 walks the frame serially
     // from location 0 at Tpad
     uint32_t fin = loc;
     bool fixed = known || !active;
-    const int rounds = (dbg & kDbgTbCap) ? 0 : 65;
+    const bool tbforce = (dbg & kDbgTbCap) != 0;
+    const int rounds = tbforce ? 0 : 65;
     bool unproven = false;
     for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
-        const bool okb = fixed || loc_top == sf;
+        const bool okb = fixed || (loc_top == sf && !tbforce);
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
         if (round == rounds) {

@@ -365,15 +365,16 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
             }
         }
         // (chains of 32 blocks: at most 31 re-walk rounds) completeness guard: a frame still
-        // unproven after the cap (VTB_DEBUG bit 17: no re-walk) is walked serially from its known
+        // unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is walked serially from its known
         // location at hi by lane 32f
         uint32_t fin = loc;
         bool fixed = known || !active;
-        const int rounds = (dbg & kDbgTbCap) ? 0 : 33;
+        const bool tbforce = (dbg & kDbgTbCap) != 0;
+        const int rounds = tbforce ? 0 : 33;
         uint64_t unproven = 0;
         for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
-            const bool ok = fixed || loc_top == sf;
+            const bool ok = fixed || (loc_top == sf && !tbforce);
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0 && uint32_t(bad >> (32 * (1 - f))) == 0) break;
@@ -829,16 +830,17 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
         }
     }
     // (chains of 32 blocks, the last known: at most 31 re-walk rounds.)  Completeness guard:
-    // a frame with a block still unproven after the cap (VTB_DEBUG bit 17: no re-walk) is traced
+    // a frame with a block still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is traced
     // back serially by lane 32f from location 0 at Tpad, the reference's own walk
     // (viterbiDecoderButterflyk1.c:200-256)
     uint32_t fin = loc;
     bool fixed = known || (dbg & 4);
-    const int rounds = (dbg & kDbgTbCap) ? 0 : 33;
+    const bool tbforce = (dbg & kDbgTbCap) != 0;
+    const int rounds = tbforce ? 0 : 33;
     uint64_t unproven = 0;
     for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
-        const bool ok = fixed || loc_top == sf;
+        const bool ok = fixed || (loc_top == sf && !tbforce);
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
         if (round == rounds) {
@@ -1011,15 +1013,16 @@ __global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__
         }
     }
     // one chain of up to 64 blocks (at most 63 re-walk rounds), with the completeness guard:
-    // unproven after the cap (VTB_DEBUG bit 17: no re-walk), lane 0 walks the frame serially
+    // unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block), lane 0 walks the frame serially
     // from location 0 at Tpad
     uint32_t fin = loc;
     bool fixed = known || !active;
-    const int rounds = (dbg & kDbgTbCap) ? 0 : 65;
+    const bool tbforce = (dbg & kDbgTbCap) != 0;
+    const int rounds = tbforce ? 0 : 65;
     bool unproven = false;
     for (int round = 0;; round++) {
         const uint32_t sfin = __shfl_down(fin, 1);
-        const bool okb = fixed || loc_top == sfin;
+        const bool okb = fixed || (loc_top == sfin && !tbforce);
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
         if (round == rounds) {

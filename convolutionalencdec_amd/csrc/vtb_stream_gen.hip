@@ -194,13 +194,14 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         unsigned fin = s;
         bool fixed = !active || start == hi;
         // (chains of G blocks: at most G - 1 re-walk rounds.)  Completeness guard: a stream with
-        // a block still unproven after the cap (VTB_DEBUG bit 17: no re-walk) is emitted by its
+        // a block still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is emitted by its
         // lane 0 alone, walking serially from its known state at hi
-        const int rounds = (table.dbg & kDbgTbCap) ? 0 : G + 1;
+        const bool tbforce = (table.dbg & kDbgTbCap) != 0;
+        const int rounds = tbforce ? 0 : G + 1;
         uint64_t unproven = 0;
         for (int round = 0;; round++) {
             const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
-            const bool ok = fixed || s_top == sf;
+            const bool ok = fixed || (s_top == sf && !tbforce);
             const uint64_t bad = ~__ballot(ok);
             if (bad == 0) break;
             if (round == rounds) {

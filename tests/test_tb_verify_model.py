@@ -24,17 +24,19 @@ import pytest
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "convolutionalencdec_amd", "csrc")
 
 
-def verify(entry_top, walk, start_exit, cap):
+def verify(entry_top, walk, start_exit, cap, force=False):
     """The kernel loop over one chain (block i's successor is i + 1; the last block is known).
     entry_top[i]: the location block i's first walk reached at its top; walk(i, loc): block i's
-    exit walked from loc; start_exit[i]: its exit from the first walk.
-    Returns (re-walk rounds used, proven, guard fired)."""
+    exit walked from loc; start_exit[i]: its exit from the first walk.  force: VTB_DEBUG bit 17
+    (no check counts, cap 0).  Returns (re-walk rounds used, proven, guard fired)."""
     n = len(entry_top)
     fin = list(start_exit)
     fixed = [False] * (n - 1) + [True]
+    if force:
+        cap = 0
     rnd = 0
     while True:
-        ok = [fixed[i] or (entry_top[i] == fin[i + 1]) for i in range(n - 1)] + [True]
+        ok = [fixed[i] or (entry_top[i] == fin[i + 1] and not force) for i in range(n - 1)] + [True]
         bad = [not o for o in ok]
         if not any(bad):
             return rnd, True, False
@@ -75,18 +77,24 @@ def test_round3_split_bound_fires_guard():
     assert verify(top, walk, ex, 65)[:2] == (61, True)
 
 
-def test_cap_zero_fires_on_any_failed_first_walk():
-    """VTB_DEBUG bit 17 (cap 0): every chain with a block whose first walk did not verify."""
+def test_forced_guard_fires_on_every_walked_chain():
+    """VTB_DEBUG bit 17: every chain with a block not known from the frame end takes the guard,
+    even one whose first walks all verified; a chain of known blocks only does not."""
     for n in (2, 32, 64):
         top, walk, ex = adversarial_chain(n, seed=n)
-        assert verify(top, walk, ex, 0) == (0, False, True)
+        assert verify(top, walk, ex, 65, force=True) == (0, False, True)
     top, walk, ex = adversarial_chain(8, seed=3)
-    assert verify([walk(i + 1, 0) if i < 7 else 0 for i in range(8)], walk, [walk(i, 0) for i in range(8)], 0)[:2] == (0, True)
+    good = [walk(i + 1, 0) if i < 7 else 0 for i in range(8)], walk, [walk(i, 0) for i in range(8)]
+    assert verify(*good, 65)[:2] == (0, True)
+    assert verify(*good, 65, force=True) == (0, False, True)
+    assert verify([0], walk, [0], 65, force=True) == (0, True, False)
 
 
 def _caps(fname):
     src = open(os.path.join(CSRC, fname)).read()
-    caps = re.findall(r"const int rounds = \((?:table\.|a\.)?dbg & kDbgTbCap\) \? 0 : ([^;]+);", src)
+    caps = re.findall(r"const int rounds = tbforce \? 0 : ([^;]+);", src)
+    assert len(re.findall(r"const bool tbforce = \((?:table\.|a\.)?dbg & kDbgTbCap\) != 0;", src)) == len(caps)
+    assert len(re.findall(r"const bool okb? = fixed \|\| \(\w+ == \w+ && !tbforce\);", src)) == len(caps)
     loops = len(re.findall(r"for \(int round = 0;; round\+\+\)", src))
     assert len(caps) == loops, (fname, caps, loops)
     assert not re.search(r"for \(int round = 0; round <", src), f"{fname}: an unguarded verification loop"

@@ -7,7 +7,7 @@
 #                            sha beside it for tools/kernel_time_summary.py)
 #   tools/gpu_r05.sh fuzz    one fuzz sweep and one fix-up sweep on this library (2,000 cases per
 #                            family), plus the fuzz sweep again with every traceback verification
-#                            allowed no re-walk round (VTB_DEBUG bit 17: the guards' slow paths)
+#                            forced to the guards' slow paths (VTB_DEBUG bit 17)
 #   tools/gpu_r05.sh stamps  PMC passes of every config line, the config lines, SQ passes of the
 #                            headline (summarised on the CPU: tools/traffic_summary.py, ...)
 set -o pipefail
@@ -45,8 +45,8 @@ for step in "$@"; do
       tail -n 1 $O/fuzz/fuzz_seed5005.log
       VTB_FIXUP_N=2000 VTB_FIXUP_SEED=5007 timeout -k 10 600 ${PYT/-x /} tests/test_gpu_split_fixup.py -m gpu -k fixup_family > $O/fuzz/fixup_seed5007.log 2>&1 || { tail -30 $O/fuzz/fixup_seed5007.log; exit 1; }
       tail -n 1 $O/fuzz/fixup_seed5007.log
-      VTB_DEBUG=131072 VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5006 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_cap0_seed5006.log 2>&1 || { tail -30 $O/fuzz/fuzz_cap0_seed5006.log; exit 1; }
-      tail -n 1 $O/fuzz/fuzz_cap0_seed5006.log ;;
+      VTB_DEBUG=131072 VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5006 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_forced_seed5006.log 2>&1 || { tail -30 $O/fuzz/fuzz_forced_seed5006.log; exit 1; }
+      tail -n 1 $O/fuzz/fuzz_forced_seed5006.log ;;
     stamps)
       timeout -k 10 900 bash tools/pmc_passes.sh head c2 c3s c3h c4 c5 || exit 1
       timeout -k 10 600 bash tools/configs.sh && cp gpurun_out/configs.jsonl $O/configs.jsonl || exit 1
