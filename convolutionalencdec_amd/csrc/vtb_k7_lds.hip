@@ -578,11 +578,12 @@ __device__ void stream_traceback(const StreamArgs& sa, uint8_t* out, size_t out_
         uint32_t fin = loc;
         bool fixed = known || !active;
         const bool tbforce = (dbg & kDbgTbCap) != 0;
+        if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
         const int rounds = tbforce ? 0 : 33;
         bool unproven = false;
         for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
-            const bool ok = fixed || (loc_top == sf && !tbforce);
+            const bool ok = fixed || loc_top == sf;
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0) break;
@@ -1350,12 +1351,13 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t fin = loc;  // survivor's location at step blk * tbb
     bool fixed = known || (dbg & 4);  // dbg bit 2 (measurement builds only): skip verification
     const bool tbforce = (dbg & kDbgTbCap) != 0;
+    if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
     const int rounds = tbforce ? 0 : (SPLIT && sp) ? 65 : 33;
     uint64_t unproven = 0;
     for (int round = 0;; round++) {
         // successor's exit (lane 31, frame A's last block, is known)
         const uint32_t sf = (SPLIT && sp) ? __shfl(fin, lane == nA - 1 ? kB0 : (lane + 1) & 63) : __shfl_down(fin, 1);
-        const bool ok = fixed || (loc_top == sf && !tbforce);
+        const bool ok = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
         if (round == rounds) {
@@ -1586,11 +1588,12 @@ __global__ __launch_bounds__(512) void k7_seg_kernel(const uint8_t* __restrict__
     uint32_t fin = loc;
     bool fixed = known || !active;
     const bool tbforce = (dbg & kDbgTbCap) != 0;
+    if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
     const int rounds = tbforce ? 0 : 65;
     bool unproven = false;
     for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
-        const bool okb = fixed || (loc_top == sf && !tbforce);
+        const bool okb = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
         if (round == rounds) {

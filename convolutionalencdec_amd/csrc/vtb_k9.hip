@@ -370,11 +370,12 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
         uint32_t fin = loc;
         bool fixed = known || !active;
         const bool tbforce = (dbg & kDbgTbCap) != 0;
+        if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
         const int rounds = tbforce ? 0 : 33;
         uint64_t unproven = 0;
         for (int round = 0;; round++) {
             const uint32_t sf = __shfl_down(fin, 1);
-            const bool ok = fixed || (loc_top == sf && !tbforce);
+            const bool ok = fixed || loc_top == sf;
             const uint64_t bad = ~__ballot(ok);
             const uint32_t badf = uint32_t(bad >> (32 * f));
             if (badf == 0 && uint32_t(bad >> (32 * (1 - f))) == 0) break;
@@ -836,11 +837,12 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
     uint32_t fin = loc;
     bool fixed = known || (dbg & 4);
     const bool tbforce = (dbg & kDbgTbCap) != 0;
+    if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
     const int rounds = tbforce ? 0 : 33;
     uint64_t unproven = 0;
     for (int round = 0;; round++) {
         const uint32_t sf = __shfl_down(fin, 1);
-        const bool ok = fixed || (loc_top == sf && !tbforce);
+        const bool ok = fixed || loc_top == sf;
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
         if (round == rounds) {
@@ -1018,11 +1020,12 @@ __global__ __launch_bounds__(512) void k9_seg_kernel(const uint8_t* __restrict__
     uint32_t fin = loc;
     bool fixed = known || !active;
     const bool tbforce = (dbg & kDbgTbCap) != 0;
+    if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
     const int rounds = tbforce ? 0 : 65;
     bool unproven = false;
     for (int round = 0;; round++) {
         const uint32_t sfin = __shfl_down(fin, 1);
-        const bool okb = fixed || (loc_top == sfin && !tbforce);
+        const bool okb = fixed || loc_top == sfin;
         const uint64_t bad = ~__ballot(okb);
         if (bad == 0) break;
         if (round == rounds) {
