@@ -367,13 +367,10 @@ def load_isa_mix(kernel, soft):
     return _stamped("isa_mix.json", f"{kernel}/{'soft' if soft else 'hard'}")
 
 
-def roofline_block(alg_bytes, avg_ms, n_avg, kern_ms, launch_ms, issue_us, state_steps, kernel, traffic=None,
-                   kernel_time=None, valu=None, mix=None):
-    """The bench line's `roofline` object.  HBM roofline of the decode kernel: algorithmic bytes
-    per launch / the average launch time avg_ms (back-to-back launches, DESIGN.md 5) against
-    8 TB/s, `traffic` = PMC-measured HBM bytes per launch.  `secondary`: the bound that holds,
-    integer VALU issue, against the 2-cycle peak and the kernel's issue-priced mix."""
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+def secondary_block(avg_ms, state_steps, kernel, valu=None, mix=None):
+    """roofline.secondary: the bound that holds, integer VALU issue.  achieved = the PMC-counted
+    wave64 VALU instructions per launch / avg_ms, against the 2-cycle peak (`frac`), the 4-cycle
+    rate (`frac_4cycle`) and the kernel's issue-priced ACS mix (`issue_priced`)."""
     sec = {"bound": "valu", "kernel": kernel,
            "note": KERNEL_NOTES.get(kernel, "see DESIGN.md 5") + "; DESIGN.md 5",
            "state_steps_per_s": round(state_steps / (avg_ms * 1e-3))}
@@ -394,6 +391,17 @@ def roofline_block(alg_bytes, avg_ms, n_avg, kern_ms, launch_ms, issue_us, state
         if ach is not None:
             ip["frac"] = round(ach / mix["priced_peak_G"], 4)
         sec["issue_priced"] = ip
+    return sec
+
+
+def roofline_block(alg_bytes, avg_ms, n_avg, kern_ms, launch_ms, issue_us, state_steps, kernel, traffic=None,
+                   kernel_time=None, valu=None, mix=None):
+    """The bench line's `roofline` object.  HBM roofline of the decode kernel: algorithmic bytes
+    per launch / the average launch time avg_ms (back-to-back launches, DESIGN.md 5) against
+    8 TB/s, `traffic` = PMC-measured HBM bytes per launch.  `secondary`: the bound that holds,
+    integer VALU issue, against the 2-cycle peak and the kernel's issue-priced mix."""
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    sec = secondary_block(avg_ms, state_steps, kernel, valu, mix)
     issue_bound = issue_us is not None and issue_us * 1e-3 >= 0.8 * avg_ms
     return {
         "bound": "hbm",

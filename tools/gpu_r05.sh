@@ -37,7 +37,7 @@ for step in "$@"; do
     prof)
       export TMPDIR=/tmp
       rm -rf $O/prof && mkdir -p $O/prof && echo "$sha" > $O/prof/lib_sha16.txt
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_bench.json 2> $O/prof.err || { tail $O/prof.err; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_bench.json 2> $O/prof.err || { tail $O/prof.err; exit 1; }
       find $O/prof -name '*kernel_stats.csv' | head -3 ;;
     fuzz)
       mkdir -p $O/fuzz
