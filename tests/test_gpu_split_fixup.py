@@ -11,7 +11,8 @@ so each path must too.
 
 * `test_case_1366_*`: the round-3 failure (fuzz seed 1017 case 1366: K=7, L = 2,966, soft,
   sigma 4, three frames; 6 wrong bits at 85-93 of frame 1).  Root cause: the split pass chains
-  up to 62 traceback blocks (frame A's 32, frame B's 2..31) but verified them in at most 33
+  up to 63 traceback blocks (frame A's nA <= 32, frame B's kB0-32..31 with kB0 = 32 + warm/48;
+  62 at warm-up 96) but verified them in at most 33
   rounds, so on a pure-noise frame kept split by the fix-up frame A's first blocks left the
   loop unverified.  Pinned on the single-frame entry and the batch entry, under every fix-up
   mode.
