@@ -214,3 +214,20 @@ def test_general_k(orc, counter, monkeypatch, which, capped):
         got = GenKDecoder(1, K, g, L).decode_device(torch.from_numpy(rx).cuda()).cpu().numpy()
         assert native.last_kernel() == which
     _check(counter, got, want, capped, which)
+
+
+# ---- random batches with every guard forced (the fuzz family of tests/test_gpu_fuzz.py) ----
+
+from test_gpu_fuzz import _cases as _fuzz_cases  # noqa: E402
+from test_gpu_fuzz import test_random_case_vs_oracle as _fuzz_case  # noqa: E402
+
+
+@pytest.mark.parametrize("case", _fuzz_cases(48, 20261105),
+                         ids=lambda c: f"{c[0]}-K{c[1]}-L{c[2]}-F{c[3]}-{'soft' if c[4] else 'hard'}")
+def test_random_batches_forced(orc, counter, monkeypatch, case):
+    """48 seeded random batches (K = 3..9, any length, 1 to 9,001 frames, clean to pure noise,
+    strided buffers) with every completeness guard forced: still bit-exact against the oracle.
+    (The whole fuzz suite with VTB_DEBUG=131072: profiles/r05/final/fuzz/.)"""
+    monkeypatch.setenv("VTB_DEBUG", str(CAP))
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    _fuzz_case(orc, case)
