@@ -142,3 +142,57 @@ def test_committed_isa_mix_covers_the_bench_configs():
         assert ent["mix"]["pk_min"] == 48 * regs and ent["loop_steps"] == 48, key
         assert 500 < ent["priced_peak_G"] < 1228.8, key
         assert len(ent["lib_sha16"]) == 16
+
+
+# ---- tools/kernel_time_summary.py (ADVICE r04): the timed window and the stamp's source ----
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import kernel_time_summary as kts  # noqa: E402
+
+
+def _spans(bursts):
+    """[(start, end)] of back-to-back 32-us dispatches in bursts separated by the given gaps."""
+    out, t = [], 0
+    for n, gap in bursts:
+        t += gap
+        for _ in range(n):
+            out.append((t, t + 32_000))
+            t += 32_000 + 500
+    return out
+
+
+def test_timed_window_skips_the_isolated_first_dispatch():
+    # bench.py: one isolated dispatch, the 5-launch warm-up burst, the 20 timed launches, the
+    # 51-launch average pass, the per-launch pass (events open ~5 us gaps)
+    sp = _spans([(1, 0), (5, 400_000), (20, 70_000), (51, 45_000)] + [(1, 6_000)] * 20)
+    assert kts.timed_window(sp, 5, 20) == 6
+    assert kts.timed_window(_spans([(5, 0), (20, 70_000)]), 5, 20) == 5
+
+
+@pytest.mark.parametrize("trace", ["profiles/r04/final/kernel_trace_bench_driver_cmd.csv",
+                                   "profiles/r05/final/kernel_trace_bench_driver_cmd.csv"])
+def test_timed_window_on_committed_traces(trace):
+    import csv
+
+    rows = [r for r in csv.DictReader(open(os.path.join(REPO, trace))) if "k7_lds_kernel" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    sp = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
+    lo = kts.timed_window(sp, 5, 20)
+    assert lo == 6  # the driver's command: dispatch 0 alone, 1-5 the warm-up, 6-25 timed
+    assert all(sp[i][0] - sp[i - 1][1] < 10_000 for i in range(lo + 1, lo + 20))
+    assert sp[lo][0] - sp[lo - 1][1] > 10_000
+
+
+def test_summary_refuses_unstamped_or_ambiguous_runs(tmp_path):
+    import subprocess
+
+    script = os.path.join(REPO, "tools", "kernel_time_summary.py")
+    (tmp_path / "a").mkdir()
+    (tmp_path / "a" / "run_kernel_stats.csv").write_text("Name,Calls,AverageNs\n")
+    r = subprocess.run([sys.executable, script, str(tmp_path), "K"], capture_output=True, text=True)
+    assert r.returncode != 0 and "lib_sha16.txt" in (r.stderr + r.stdout)
+    (tmp_path / "b").mkdir()
+    (tmp_path / "b" / "run_kernel_stats.csv").write_text("Name,Calls,AverageNs\n")
+    r = subprocess.run([sys.executable, script, str(tmp_path), "K"], capture_output=True, text=True)
+    assert r.returncode != 0 and "exactly one run" in (r.stderr + r.stdout)
