@@ -1086,6 +1086,419 @@ __global__ __launch_bounds__(64) void k9_kernel(const uint8_t* __restrict__ in, 
     }
 }
 
+// ---------------- one frame per wave (k9s) ----------------
+//
+// A batch of F frames gives the pair kernel F / 2 waves: 2 per SIMD at config C4's 4,096, where
+// the SIMD still idles (VALU active 78 % of its cycles; 4 waves per SIMD of the same kernel run
+// +15 % faster per wave-step, profiles/r05/pricing/k9_waves_ab.jsonl).  Here every wave decodes
+// one frame, so the same batch fills 4 waves per SIMD with the same work per state-step.
+//
+// Layout: location l = 128 h + 64 r + lambda -- bits 0..5 lane bits (lane_of, as k9_pair), bit 6
+// the register M[r] (r = 0, 1), bit 7 the u16 half h.  In l' = rev8(l) numbering h is bit 0, r
+// bit 1 and rev6(lambda) bits 2..7, so a survivor column of 16 steps is 256 u16 words at byte 2 l'
+// (512 B; the word of register r at 8 rev6(lambda) + 4 r holds h = 0 in its low half), and a
+// window's two decisions (l' bits t mod 8, t mod 8 + 1) are address bits 1 + t mod 8 and above.
+// Per step the butterfly partner is the other half (p = 7: one v_pk_add_u16 with the source
+// halves swapped), the other register (p = 6), a v_permlane32/16_swap (p = 5, 4) or DPP (3..0).
+//
+// Branch metrics: the pair kernel's ring with both halves from this frame.  Column k = c + 4R
+// of row t holds in its low half the value of location l (upper state label c, R = bit p of l)
+// and in its high half that of l ^ 128:
+//  * t mod 8 = ph >= 1: l ^ 128's upper state is l's with bit ph - 1 flipped, whose label is
+//    c ^ d(ph) (labels are linear in the state: checked on the host, k9s_dpack); the staging
+//    lane computes the high half from its input with the coded bits in d(ph) complemented;
+//  * ph = 0 (p = 7): l and l ^ 128 are the butterfly itself, same c, R flipped: the tie bit goes
+//    into the other half (tieE / tieT below).
+constexpr int kColS = 512;  // survivor column: 256 u16 words per 16 steps
+constexpr uint32_t kDbgK9Pair = 1u << 18;  // VTB_DEBUG bit 18 (exact): K=9 frames on the pair kernel
+
+int tb_block_s(int Tq) {
+    const int per = (Tq + 63) / 64;  // 64 blocks per frame, multiple of 48 steps
+    return (per + 47) / 48 * 48;
+}
+int region0_s(int Tq) {  // table ring, later the decoded bytes of the frame
+    const int r = 8 * tb_block_s(Tq) > kRingBytes ? 8 * tb_block_s(Tq) : kRingBytes;
+    return (r + 255) / 256 * 256;
+}
+size_t ws_wave_bytes_s(int Tq) { return (size_t)kColS * (t_pad(Tq) / 16); }
+
+// Candidates of one step for the two registers (as candidates<P>).
+template <int P>
+__device__ __forceinline__ void candidates_s(uint32_t (&M)[2], const uint2 (&vw)[2], uint32_t (&A)[2], uint32_t (&B)[2]) {
+    if constexpr (P == 7) {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            A[r] = M[r] + vw[r].x;
+            asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(B[r]) : "v"(M[r]), "v"(vw[r].y));
+        }
+    } else if constexpr (P == 6) {
+        A[0] = M[0] + vw[0].x, B[0] = M[1] + vw[0].y;
+        A[1] = M[1] + vw[1].x, B[1] = M[0] + vw[1].y;
+    } else if constexpr (P == 5 || P == 4) {
+        // s_nop: one wait state between the last VALU write of M[r] and its swap (the adds may be
+        // fewer than the hazard needs when the compiler puts M[1]'s write right before), and
+        // between the last swap and the first read of a result
+        if constexpr (P == 5) {
+            asm volatile(
+                "v_add_u32 %0, %2, %4\n\tv_add_u32 %1, %3, %5\n\ts_nop 0\n\t"
+                "v_permlane32_swap_b32 %2, %2\n\tv_permlane32_swap_b32 %3, %3\n\ts_nop 0"
+                : "=&v"(A[0]), "=&v"(A[1]), "+v"(M[0]), "+v"(M[1])
+                : "v"(vw[0].x), "v"(vw[1].x));
+        } else {
+            asm volatile(
+                "v_add_u32 %0, %2, %4\n\tv_add_u32 %1, %3, %5\n\ts_nop 0\n\t"
+                "v_permlane16_swap_b32 %2, %2\n\tv_permlane16_swap_b32 %3, %3\n\ts_nop 0"
+                : "=&v"(A[0]), "=&v"(A[1]), "+v"(M[0]), "+v"(M[1])
+                : "v"(vw[0].x), "v"(vw[1].x));
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) B[r] = M[r] + vw[r].y;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            A[r] = M[r] + vw[r].x;
+            if constexpr (P == 3) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x128, 0xF, 0xF, true) + vw[r].y;  // row_ror:8
+            if constexpr (P == 2) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x141, 0xF, 0xF, true) + vw[r].y;  // XOR 7
+            if constexpr (P == 1) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0x4E, 0xF, 0xF, true) + vw[r].y;   // XOR 2
+            if constexpr (P == 0) B[r] = __builtin_amdgcn_update_dpp(0u, M[r], 0xB1, 0xF, 0xF, true) + vw[r].y;   // XOR 1
+        }
+    }
+}
+
+// 48 traceback steps over [tlo, tlo + 48), newest first (tb_body / tb_body8 in the k9s column
+// layout): cb the byte offset of the block's first survivor column (bits 0..8 clear), la = 2 l'
+// of the survivor's location.  Returns the 48 decoded bits, bit 0 = step tlo.
+template <bool SOFT>
+__device__ __forceinline__ uint64_t tbs_body(uint32_t cb, uint32_t& la, uint64_t gbase) {
+    uint32_t a = cb | la;
+    uint64_t bits = 0;
+    if constexpr (SOFT) {
+#pragma unroll
+        for (int j = 0; j < 24; j++) {
+            const int todd = 47 - 2 * j;
+            if (j % 4 == 0) bits |= uint64_t((a >> 1) & 0xFFu) << (8 * (5 - j / 4));
+            const int wi = (todd & 15) >> 1, sh = 8 * (wi & 1) + 2 * (wi >> 1);
+            uint32_t v;
+            asm volatile("global_load_ushort %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"((todd >> 4) * kColS));
+            const int pos = ((todd - 1) & 7) + 1;
+            const uint32_t fld = pos >= sh ? (v << (pos - sh)) : (v >> (sh - pos));
+            a = (a & ~(3u << pos)) | (fld & (3u << pos));
+        }
+    } else {
+#pragma unroll
+        for (int k = 5; k >= 0; k--) {
+            bits |= uint64_t((a >> 1) & 0xFFu) << (8 * k);
+            uint32_t v;
+            asm volatile("global_load_ubyte %0, %1, %2 offset:%3\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(v) : "v"(a), "s"(gbase), "i"(kColS * (k >> 1) + (k & 1)));
+            a = (a & ~0x1FEu) | (v << 1);
+        }
+    }
+    la = a & 0x1FEu;
+    return bits;
+}
+
+// One frame (index fr) per wave, survivors in workspace slot `slot`.  dpack: d(ph) of the
+// header, 2 bits per phase.
+template <bool SOFT>
+__device__ __forceinline__ void k9_single(const uint8_t* __restrict__ in, size_t in_stride, uint8_t* __restrict__ out,
+                                          size_t out_stride, int T, int L, int delta, int Tq, int Tpad, int tbb,
+                                          int dbg, uint8_t* __restrict__ ws, size_t ws_wave, size_t fr, size_t slot,
+                                          const uint32_t (&off)[2][8], uint32_t dpack, uint32_t* hits) {
+    constexpr uint32_t Q = SOFT ? 255 : 1;
+    using H = Hist<SOFT>;
+    constexpr uint32_t B4 = H::SC * 8 * 2 * Q;  // as k9_pair (NB = 2)
+    extern __shared__ uint4 smem4[];
+    uint8_t* tab = reinterpret_cast<uint8_t*>(smem4);
+    const int lane = int(threadIdx.x);
+    const uint64_t gbase = uniform64(reinterpret_cast<uint64_t>(ws + slot * ws_wave));
+    const uint32_t lam = lane_of(uint32_t(lane));
+
+    // Table staging: lane r < 48 builds ring row r of a chunk (k9_pair), both halves from this
+    // frame's input (header: the high half's coded bits complemented by d(ph), its tie bit in
+    // the other half at ph = 0).
+    const int srow = lane < kCh ? lane : lane - kCh;
+    const int sph = srow & 7;
+    const uint32_t d = (dpack >> (2 * sph)) & 3u;
+    const uint32_t xmask = SOFT ? ((d & 1u) ? 0xFFu : 0u) | ((d & 2u) ? 0xFF00u : 0u) : d;
+    const uint32_t tie16 = 1u << (srow & (H::HB - 1));
+    const uint32_t tieE = sph == 0 ? tie16 << 16 : 0u, tieT = sph == 0 ? tie16 : tie16 * kR1;
+    const uint64_t base = uniform64(reinterpret_cast<uint64_t>(in + fr * in_stride));
+    auto load_raw = [&](int c, uint32_t& ra) {
+        int t = c * kCh + srow - delta;
+        t = t < 0 ? 0 : (t < T ? t : T - 1);
+        if constexpr (SOFT)
+            asm volatile("global_load_ushort %0, %1, %2" : "=v"(ra) : "v"(2u * uint32_t(t)), "s"(base));
+        else
+            asm volatile("global_load_ubyte %0, %1, %2" : "=v"(ra) : "v"(uint32_t(t)), "s"(base));
+    };
+    auto stage_compute = [&](uint32_t ra, uint32_t (&e)[4], uint32_t (&et)[4]) {
+        const uint32_t rb = ra ^ xmask;
+        uint32_t q0 = __builtin_amdgcn_perm(rb, ra, 0x0C040C00u);
+        uint32_t q1 = __builtin_amdgcn_perm(rb, ra, 0x0C050C01u);
+        if constexpr (!SOFT) {
+            q1 = (q0 >> 1) & kR1;
+            q0 &= kR1;
+        }
+        q0 <<= H::HB;
+        q1 <<= H::HB;
+        constexpr uint32_t QQ = H::SC * Q * kR1;
+        e[0] = q0 + q1, e[1] = (QQ + q1) - q0, e[2] = 2 * QQ - e[1], e[3] = 2 * QQ - e[0];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            et[k] = e[k] + tieT;
+            e[k] += tieE;
+        }
+    };
+    const uint32_t wbase0 = 8u * uint32_t(srow), wbase1 = wbase0 + 24u * kCol, wbase2 = wbase0 + 48u * kCol;
+    auto stage_write = [&](int c, const uint32_t (&e)[4], const uint32_t (&et)[4]) {
+#define VTB_W2(base, k, v, w)                                                                         \
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(v), "v"(w),        \
+                 "i"(2 * kCol * ((k) % 3)), "i"(2 * kCol * ((k) % 3) + 1) : "memory");
+        VTB_W2(wbase0, 0, e[0], et[3]) VTB_W2(wbase0, 1, e[1], et[2]) VTB_W2(wbase0, 2, e[2], et[1])
+        VTB_W2(wbase1, 3, e[3], et[0]) VTB_W2(wbase1, 4, et[0], e[3]) VTB_W2(wbase1, 5, et[1], e[2])
+        VTB_W2(wbase2, 6, et[2], e[1]) VTB_W2(wbase2, 7, et[3], e[0])
+#undef VTB_W2
+        // own-keeping rows (k9_pair): the start step of odd T, for hard input the padding steps
+        const bool pad_row = !SOFT && (c + 1) * kCh > Tq && c * kCh + srow >= Tq;
+        if ((c == 0 && srow < delta) || pad_row) {
+            uint2* col = reinterpret_cast<uint2*>(tab) + srow;
+            constexpr uint32_t PADW = H::SC * ((SOFT ? 2 : 16) * Q + 1) * kR1;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                col[k * kCol] = make_uint2(tieE, PADW + tieT);
+                col[(4 + k) * kCol] = make_uint2(tieT, PADW + tieE);
+            }
+        }
+    };
+
+    // start metrics (k9_pair): location 0 (register 0, low half, lane 0) at B4, the rest B4 + Q
+    uint32_t M[2];
+    M[0] = (lane == 0) ? B4 | ((B4 + H::SC * Q) << 16) : (B4 + H::SC * Q) * kR1;
+    M[1] = (B4 + H::SC * Q) * kR1;
+    uint32_t ra;
+    {
+        uint32_t e[4], et[4];
+        load_raw(0, ra);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra));
+        stage_compute(ra, e, et);
+        stage_write(0, e, et);
+    }
+    uint2 buf[kRS][2];
+#pragma unroll
+    for (int s = 0; s < kAH; s++)
+#pragma unroll
+        for (int r = 0; r < 2; r++) buf[s][r] = *reinterpret_cast<const uint2*>(tab + off[r][s] + 8 * s);
+
+    const uint32_t wlane = 8u * rev6(lam);  // survivor word byte offset of the lane within a column
+    uint32_t dd = 0, m_prev[2] = {0, 0}, pw[2][4] = {}, se[4], set[4];
+    const int tacs = (dbg & 2) ? 0 : Tpad;
+    for (int t0 = 0; t0 < tacs; t0 += kCh) {
+        const int c0 = t0 / kCh;
+        const uint32_t gvo = uint32_t(kColS) * uint32_t(t0 >> 4) + wlane;
+        static_for(std::make_integer_sequence<int, kCh>{}, [&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            constexpr int PH = I % 8;
+            if constexpr (I == 0) load_raw(c0 + 1, ra);  // next chunk's raw input
+            if constexpr (I == 20) {
+                // one survivor store batch (step 15, two stores) was issued after the load
+                asm volatile("s_waitcnt vmcnt(2)" : "+v"(ra));
+                stage_compute(ra, se, set);
+            }
+            if constexpr (I == kCh - kAH) stage_write(c0 + 1, se, set);
+            // renormalisation against location 0 (low half of lane 0's M[0]), both halves
+            constexpr bool RN_READ = SOFT ? (I % 12) == 10 : I == 40;
+            constexpr bool RN_APPLY = SOFT ? (I % 12) == 11 : I == 47;
+            if constexpr (RN_READ) {
+                const uint32_t ref = __builtin_amdgcn_readfirstlane(M[0]) & 0xFFFFu;
+                dd = B4 * kR1 - ref * kR1;
+            }
+            uint32_t A[2], Bc[2];
+            candidates_s<7 - PH>(M, buf[I % kRS], A, Bc);
+            {
+                constexpr int IN = (I + kAH) % kCh, PN = IN % 8;
+#pragma unroll
+                for (int r = 0; r < 2; r++)
+                    buf[(I + kAH) % kRS][r] = *reinterpret_cast<const uint2*>(tab + off[r][PN] + 8 * IN);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; r++) M[r] = pk_min(A[r], Bc[r]);
+            if constexpr (!SOFT && (I & 7) == 7) {
+                // octet history bytes: [h0 oct 0, h0 oct 1, h1 oct 0, h1 oct 1] per 16 steps
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    if constexpr ((I & 15) == 7) m_prev[r] = M[r];
+                    else pw[r][0] = __builtin_amdgcn_perm(M[r], m_prev[r], 0x06020400u);
+                    M[r] = RN_APPLY ? ((M[r] & ~H::MASK) + dd) : (M[r] & ~H::MASK);
+                }
+                if constexpr ((I & 15) == 15) {
+                    constexpr int W = I >> 4;
+                    gstore<W * kColS>(gvo, pw[0][0], gbase);
+                    gstore<W * kColS + 4>(gvo, pw[1][0], gbase);
+                }
+            }
+            if constexpr (SOFT && (I & 1)) {
+                constexpr int w = (I & 15) >> 1;
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    if constexpr (w & 1) pw[r][w >> 1] = __builtin_amdgcn_perm(M[r], m_prev[r], 0x06020400u);
+                    else m_prev[r] = M[r];
+                    M[r] = RN_APPLY ? ((M[r] & ~H::MASK) + dd) : (M[r] & ~H::MASK);
+                }
+                if constexpr ((I & 15) == 15) {
+                    constexpr int W = I >> 4;
+                    uint32_t z[2];
+#pragma unroll
+                    for (int r = 0; r < 2; r++) {
+                        z[r] = bfi_op(0x03030303u, pw[r][0], pw[r][1] << 2);
+                        z[r] = bfi_op(0x0F0F0F0Fu, z[r], pw[r][2] << 4);
+                        z[r] = bfi_op(0x3F3F3F3Fu, z[r], pw[r][3] << 6);
+                    }
+                    gstore<W * kColS>(gvo, z[0], gbase);
+                    gstore<W * kColS + 4>(gvo, z[1], gbase);
+                }
+            }
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // Soft input, padding steps [Tq, Tpad): own-keeping survivor bits (k9_pair), per half
+    if (SOFT && !(dbg & 2)) {
+        uint32_t* wsw = reinterpret_cast<uint32_t*>(ws + slot * ws_wave);
+        for (int g = Tq >> 4; g < (Tpad >> 4); g++) {
+            const int w0 = Tq > 16 * g ? (Tq - 16 * g) >> 1 : 0;  // first padding window of the word
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const uint32_t lp = (rev6(lam) << 2) | (uint32_t(r) << 1);  // l' of the low half
+                uint32_t own = 0, mask = 0;
+                for (int w = w0; w < 8; w++) {
+                    const int sh = 8 * (w & 1) + 2 * (w >> 1);
+                    own |= ((lp >> (2 * (w & 3))) & 3u) << sh;
+                    own |= (((lp | 1u) >> (2 * (w & 3))) & 3u) << (sh + 16);
+                    mask |= 3u << sh;
+                }
+                mask |= mask << 16;
+                uint32_t* p = wsw + (kColS / 4) * g + (wlane >> 2) + r;
+                *p = (*p & ~mask) | (own & mask);
+            }
+        }
+    }
+    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (dbg & 1) return;
+
+    // ---------------- traceback: verified block-parallel chains, 64 blocks ----------------
+    const int blk = lane;
+    uint8_t* ob = tab;
+    const int top = (blk + 1) * tbb;
+    const int start_full = top + kTbWarm;
+    const int start = min(start_full, Tpad);
+    const bool known = start >= Tq;
+    const int nbody = (dbg & 8) ? 1 : (kTbWarm + tbb) / 48;
+    uint32_t loc = 0, loc_top = 0;
+    for (int g = 0; g < nbody; g++) {
+        const int tlo = start_full - 48 * (g + 1);
+        if (g == kTbWarm / 48) loc_top = loc;
+        if (tlo < start) {
+            const uint64_t bits = tbs_body<SOFT>(uint32_t(kColS) * uint32_t(tlo >> 4), loc, gbase);
+            if (g >= kTbWarm / 48) put_bits48(ob, tlo, bits);
+        }
+    }
+    // (chains of at most 64 blocks, the last known: at most 63 re-walk rounds.)  Completeness
+    // guard as k9_pair: a frame with a block still unproven after the cap (VTB_DEBUG bit 17: every
+    // chain with a walked block) is traced back serially by lane 0 from location 0 at Tpad
+    uint32_t fin = loc;
+    bool fixed = known || (dbg & 4);
+    const bool tbforce = (dbg & kDbgTbCap) != 0;
+    if (tbforce) loc_top = ~0u;  // (bit 17: no check passes)
+    const int rounds = tbforce ? 0 : 65;
+    uint64_t unproven = 0;
+    for (int round = 0;; round++) {
+        const uint32_t sf = __shfl_down(fin, 1);
+        const bool ok = fixed || loc_top == sf;
+        const uint64_t bad = ~__ballot(ok);
+        if (bad == 0) break;
+        if (round == rounds) {
+            unproven = bad;
+            break;
+        }
+        const bool succ_proven = blk == 63 || (bad >> (blk + 1)) == 0;
+        if (!ok && succ_proven) {
+            loc = sf;
+            for (int g = kTbWarm / 48; g < nbody; g++) {
+                const int tlo = start_full - 48 * (g + 1);
+                put_bits48(ob, tlo, tbs_body<SOFT>(uint32_t(kColS) * uint32_t(tlo >> 4), loc, gbase));
+            }
+            fin = loc;
+            fixed = true;
+        }
+    }
+    if (blk == 0 && unproven != 0) {
+        note_guard(hits);
+        uint32_t l = 0;
+        for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48)
+            put_bits48(ob, tlo, tbs_body<SOFT>(uint32_t(kColS) * uint32_t(tlo >> 4), l, gbase));
+    }
+    __syncthreads();
+
+    // copy out; with delta = 1 kernel step t' is input step t' - 1 (shift the stream one bit)
+    const int nbytes = (L + 7) >> 3;
+    for (int j = lane; j < nbytes; j += 64) {
+        const uint8_t v = delta ? uint8_t((ob[j] << 1) | (ob[j + 1] >> 7)) : ob[j];
+        out[fr * out_stride + j] = v;
+    }
+}
+
+// One wave per frame, for batches the CUs hold in one round (launch_k9).
+template <bool SOFT>
+__global__ __launch_bounds__(64) void k9s_kernel(const uint8_t* __restrict__ in, size_t in_stride,
+                                                 uint8_t* __restrict__ out, size_t out_stride, int T, int L, int delta,
+                                                 int Tq, int Tpad, int tbb, int dbg, Launch table,
+                                                 uint8_t* __restrict__ ws, size_t ws_wave, uint32_t dpack) {
+    uint32_t off[2][8];
+    const uint32_t lam = lane_of(threadIdx.x);
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int ph = 0; ph < 8; ph++) {
+            const int l = r * 64 + int(lam), p = 7 - ph;
+            off[r][ph] = 8u * kCol * (table.symm[rotl8(l & ~(1 << p), ph)] + 4u * ((l >> p) & 1u));
+        }
+    k9_single<SOFT>(in, in_stride, out, out_stride, T, L, delta, Tq, Tpad, tbb, dbg, ws, ws_wave, blockIdx.x,
+                    blockIdx.x, off, dpack, table.guard_hits);
+}
+
+// d(ph) of the k9s header packed 2 bits per phase, or false if the code's butterfly labels are
+// not linear in the state (symm[s ^ e] = symm[s] ^ d for every s): then the pair kernel runs.
+bool k9s_dpack(const Launch& a, uint32_t& dpack) {
+    dpack = 0;
+    for (int ph = 1; ph < 8; ph++) {
+        const int e = 1 << (ph - 1);
+        const int d = a.symm[e] ^ a.symm[0];
+        if (d > 3) return false;
+        for (int s = 0; s < 128; s++)
+            if ((a.symm[s ^ e] ^ a.symm[s]) != d) return false;
+        dpack |= uint32_t(d) << (2 * ph);
+    }
+    return true;
+}
+
+// k9s runs a batch the CUs hold in one round (one wave per frame, resident waves and 1 GiB of
+// survivor slots); a larger batch goes to the persistent pair kernel, whose waves carry two
+// frames each: a persistent k9s grid leaves its last round part-empty (16,384 soft frames: 0.345
+// ms against the pair kernel's 0.309, profiles/r05/k9s/ab.jsonl).  False also for codes whose
+// labels are not linear in the state (k9s_dpack) and under VTB_DEBUG bit 18.
+bool k9s_use(const Launch& a, uint32_t& dpack) {
+    const int Tq = a.T + (a.T & 1);
+    if ((a.dbg & kDbgK9Pair) || (size_t)region0_s(Tq) > 64 * 1024 || !k9s_dpack(a, dpack)) return false;
+    auto kern = a.soft ? k9s_kernel<true> : k9s_kernel<false>;
+    const int per_cu = resident_per_cu(reinterpret_cast<const void*>(kern), (size_t)region0_s(Tq));
+    const size_t resident = size_t(per_cu > 0 ? per_cu : 8) * size_t(a.cus > 0 ? a.cus : 1);
+    const size_t cap = (size_t(1) << 30) / ws_wave_bytes_s(Tq);
+    return a.frames <= resident && a.frames <= cap;
+}
+
 // Grid: the frame pairs, at most what the CUs hold at once and at most 1 GiB of survivor
 // slots (one per wave).
 size_t grid_waves(const Launch& a, int Tq, int NB = 2) {
@@ -1181,6 +1594,8 @@ bool k9_supported(const Launch& a) {
 
 size_t k9_workspace_bytes(const Launch& a) {
     const int Tq = a.T + (a.T & 1);
+    uint32_t dpack;
+    if (k9s_use(a, dpack)) return a.frames * ws_wave_bytes_s(Tq);
     return grid_waves(a, Tq) * ws_wave_bytes(Tq);
 }
 
@@ -1232,6 +1647,15 @@ hipError_t launch_k9(const Launch& a) {
     if (a.frames == 0) return hipSuccess;
     if (!a.ws) return hipErrorInvalidValue;
     const int delta = a.T & 1, Tq = a.T + delta;
+    uint32_t dpack;
+    if (k9s_use(a, dpack)) {
+        note_kernel("k9s");
+        hipLaunchKernelGGL(a.soft ? k9s_kernel<true> : k9s_kernel<false>, dim3(unsigned(a.frames)), dim3(64),
+                           (size_t)region0_s(Tq), a.stream, a.in, a.in_stride, a.out, a.out_stride, a.T, a.L, delta,
+                           Tq, t_pad(Tq), tb_block_s(Tq), a.dbg, a, static_cast<uint8_t*>(a.ws),
+                           ws_wave_bytes_s(Tq), dpack);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)region0(Tq);
     const size_t grid = grid_waves(a, Tq);
     auto kern = grid < (a.frames + 1) / 2 ? (a.soft ? k9_kernel<true, true> : k9_kernel<false, true>)
