@@ -403,7 +403,7 @@ const char* vtb_version(void) { return VTB_VERSION_STRING; }
 
 // Testing only (not in include/viterbi_amd.h): the kernel instance of the calling thread's last
 // decode launch ("k7_lds", "k7_lds_loop", "k7_lds_split", "k7_global", "k7_global_loop",
-// "k7_split_loop", "k9", "k9_loop", "lds_path", "k7_seg", "k9_seg", "k7_stream", "k9_stream"),
+// "k7_split_loop", "k9", "k9_loop", "k9s", "lds_path", "k7_seg", "k9_seg", "k7_stream", "k9_stream"),
 // "" before the first.
 const char* vtb_debug_last_kernel(void) { return vtb::last_kernel(); }
 

@@ -73,7 +73,8 @@ void set_debug_tstamp(unsigned long long* p);
 //   13 full last chunk, 14 no in-wave split fix-up, 15 fix-up on every split frame, 16 fix-up
 //   checkpoints never match, 17 forced completeness guards (every traceback chain with a block not
 //   known from the frame end skips its checks and re-walks and takes the guard's exact slow
-//   path).
+//   path), 18 K=9 frames on the pair kernel (two frames per wave) where one frame per wave (k9s)
+//   would run.
 // Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
 //   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE
 //   build (tools/build_variants.sh) honours them; the shipped library masks them off.

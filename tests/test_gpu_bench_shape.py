@@ -82,10 +82,11 @@ def test_other_ranks_shards_bit_exact(orc, rank):
 
 
 def test_c4_k9_bench_batch_bit_exact(orc):
-    """Config C4 as bench.py --K 9 --hard runs it (4,096 x 1,024, the K=9 frame kernel)."""
+    """Config C4 as bench.py --K 9 --hard runs it (4,096 x 1,024, the K=9 kernel with one frame
+    per wave)."""
     code = bench.CODES[9]
     F, L = 4096, 1024
     _, rx, got, kernel = bound_decode(code, F, L, False, rank=0)
-    assert kernel == "k9", kernel
+    assert kernel == "k9s", kernel
     want = orc.decode(code[0], code[1], rx, L, soft=False)
     assert (got == want).all()

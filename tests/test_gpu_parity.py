@@ -20,7 +20,9 @@ from convolutionalencdec_amd import ConvCode, ViterbiDecoder, decode_multi, nati
 # (K=9, survivors in a global workspace), "lds" (every K).
 # "k7s": the K=7 persistent split kernel (one frame per wave as two halves, unconverged frames
 # re-decoded from a list by the global variant) wherever it applies.
-KERNELS = ("auto", "k7", "gws", "k7s", "k9", "lds")
+# "k9p": the K=9 pair kernel (two frames per wave) also for the batches "k9" / "auto" decode one
+# frame per wave (k9s; VTB_DEBUG bit 18).
+KERNELS = ("auto", "k7", "gws", "k7s", "k9", "k9p", "lds")
 
 
 class Kern(str):
@@ -28,7 +30,10 @@ class Kern(str):
         assert K in KS_OF.get(str(self), (K,)), (self, K)  # (combinations are generated valid)
 
 
-KS_OF = {"k7": (7,), "gws": (7,), "k7s": (7,), "k9": (9,)}  # kernel families tied to one K
+KS_OF = {"k7": (7,), "gws": (7,), "k7s": (7,), "k9": (9,), "k9p": (9,)}  # kernel families tied to one K
+
+
+K9_PAIR = 1 << 18
 
 
 def kernels_for(K):
@@ -55,6 +60,9 @@ def gpu_present():
 def kernel(request, monkeypatch):
     if request.param == "auto":
         monkeypatch.delenv("VTB_KERNEL", raising=False)
+    elif request.param == "k9p":
+        monkeypatch.setenv("VTB_KERNEL", "k9")
+        monkeypatch.setenv("VTB_DEBUG", str(K9_PAIR))
     else:
         monkeypatch.setenv("VTB_KERNEL", request.param)
     return Kern(request.param)

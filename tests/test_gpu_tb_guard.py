@@ -34,6 +34,7 @@ from convolutionalencdec_amd import ConvCode, GenKDecoder, ViterbiDecoder, Viter
 CAP = 1 << 17       # VTB_DEBUG: every verified chain takes the completeness guard's slow path
 NO_SPLIT = 1 << 8   # VTB_DEBUG: never split frames across the halves of a wave
 SEG_OFF = 1 << 10   # VTB_DEBUG: no single-frame SEG kernel
+K9_PAIR = 1 << 18   # VTB_DEBUG: K=9 frames on the pair kernel (not one frame per wave)
 
 
 @pytest.fixture(scope="module")
@@ -100,8 +101,11 @@ FRAME_CASES = [
     ("k7_global_soft", 7, 1024, 64, True, 0, "gws", "k7_global"),
     ("k7_global_hard_hybrid", 7, 1024, 64, False, 0, "gws", "k7_global"),
     ("k7_global_loop", 7, 512, 8192, True, 0, "gws", "k7_global_loop"),
-    ("k9_soft", 9, 1024, 64, True, 0, None, "k9"),
-    ("k9_hard", 9, 1001, 33, False, 0, None, "k9"),
+    ("k9s_soft", 9, 1024, 64, True, 0, None, "k9s"),
+    ("k9s_hard", 9, 1001, 33, False, 0, None, "k9s"),
+    ("k9s_long", 9, 16383, 5, True, 0, None, "k9s"),
+    ("k9_soft", 9, 1024, 64, True, K9_PAIR, None, "k9"),
+    ("k9_hard", 9, 1001, 33, False, K9_PAIR, None, "k9"),
     ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
     ("lds_path_k5", 5, 512, 64, False, 0, None, "lds_path"),
     ("lds_path_k7_soft", 7, 700, 16, True, 0, "lds", "lds_path"),

@@ -119,7 +119,10 @@ def test_every_loop_cap_covers_its_chain():
     assert "if (t1 > 32 * kChunk) return false;" in src and "warm >= kChunk" in src
     # stream_traceback: 32 blocks per frame; k7_seg_kernel: one chain over the 64 lanes
     k9 = _caps("vtb_k9.hip")
-    assert k9 == ["33", "33", "65"]  # stream (32 blocks), frame pair (32 per frame), SEG (64)
+    # stream (32 blocks), frame pair (32 per frame), SEG (64), one frame per wave (k9s: 64 blocks)
+    assert k9 == ["33", "33", "65", "65"]
+    src9 = open(os.path.join(CSRC, "vtb_k9.hip")).read()
+    assert "const int per = (Tq + 31) / 32;" in src9 and "const int per = (Tq + 63) / 64;" in src9
     assert _caps("vtb_genk.hip") == ["65"]  # one chain over the 64 lanes
     assert _caps("vtb_lds_path.hip") == ["G + 1"]  # G lanes (blocks) per frame
     assert _caps("vtb_stream_gen.hip") == ["G + 1"]

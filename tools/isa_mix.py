@@ -39,6 +39,7 @@ PLAIN = re.compile(r"^v_(add|sub|subrev|and|or|xor|not|lshlrev|lshrrev|ashrrev|l
 # note_kernel name -> (object, symbol template, metric registers per lane)
 K7 = "_ZN3vtb12_GLOBAL__N_113k7_lds_kernelILb{S}ELb{GS}ELb0ELb{LOOP}ELb{SPLIT}ELb0ELi2EEEvPKhmPhmiiiiimiNS_6LaunchES4_mNS_10StreamArgsE"
 K9 = "_ZN3vtb12_GLOBAL__N_19k9_kernelILb{S}ELb{LOOP}ELb0ELi2EEEvPKhmPhmiiiiiimiNS_6LaunchES4_mNS_10StreamArgsE"
+K9S = "_ZN3vtb12_GLOBAL__N_110k9s_kernelILb{S}EEEvPKhmPhmiiiiiiiNS_6LaunchES4_mj"
 KERNELS = {
     "k7_lds": ("vtb_k7_lds.o", K7, dict(GS=0, LOOP=0, SPLIT=0), 1),
     "k7_lds_loop": ("vtb_k7_lds.o", K7, dict(GS=0, LOOP=1, SPLIT=0), 1),
@@ -48,6 +49,7 @@ KERNELS = {
     "k7_global_loop": ("vtb_k7_lds.o", K7, dict(GS=1, LOOP=1, SPLIT=0), 1),
     "k9": ("vtb_k9.o", K9, dict(LOOP=0), 4),
     "k9_loop": ("vtb_k9.o", K9, dict(LOOP=1), 4),
+    "k9s": ("vtb_k9.o", K9S, {}, 2),
 }
 
 
