@@ -26,7 +26,7 @@ import os
 import statistics
 
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DECODERS = ("k7_lds_kernel", "k9_kernel", "lds_path")
+DECODERS = ("k7_lds_kernel", "k9_kernel", "k9s_kernel", "lds_path")
 
 
 def timed_window(span, warmup, steps, gap_ns=10_000):

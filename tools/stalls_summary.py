@@ -12,7 +12,7 @@ note = sys.argv[3] if len(sys.argv) > 3 else ""
 acc = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
+        if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "k9s_kernel", "lds_path")):
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: round(sum(v) / len(v)) for k, v in acc.items()}
 wc, waves = m["SQ_WAVE_CYCLES"], m["SQ_WAVES"]

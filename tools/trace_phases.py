@@ -6,7 +6,7 @@ The bench issues, on one stream, one launch from ViterbiDecoder.bind (validation
 nothing between them), K launches with an event after each (the untimed per-launch pass) and
 then the host-path launches.  Prints per phase: count, mean / min / median / max duration (us)
 and the mean gap before each launch, for the decoder kernel (the dispatches whose name holds
-`k7_lds_kernel`, `k9_kernel` or `lds_path`)."""
+`k7_lds_kernel`, `k9_kernel`, `k9s_kernel` or `lds_path`)."""
 import argparse
 import csv
 import json
@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace))
-            if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path"))]
+            if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "k9s_kernel", "lds_path"))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     st = np.array([int(r["Start_Timestamp"]) for r in rows], np.int64)
     en = np.array([int(r["End_Timestamp"]) for r in rows], np.int64)

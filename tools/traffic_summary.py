@@ -35,7 +35,7 @@ def mean_counter(d, name):
     per = {}
     for r in csv.DictReader(open(os.path.join(root, d, "run_counter_collection.csv"))):
         # the decoder's dispatches only (not the device frame generator's or runtime copies)
-        if r["Counter_Name"] == name and any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
+        if r["Counter_Name"] == name and any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "k9s_kernel", "lds_path")):
             per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return sum(sum(v) / len(v) for v in per.values()), max(len(v) for v in per.values())
 
@@ -68,7 +68,7 @@ if os.path.exists(os.path.join(root, "pmc_valu", "run_counter_collection.csv")):
     kt = os.path.join(root, "pmc_valu", "run_kernel_trace.csv")
     durs = {}
     for r in csv.DictReader(open(kt)):
-        if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "lds_path")):
+        if any(k in r["Kernel_Name"] for k in ("k7_lds_kernel", "k9_kernel", "k9s_kernel", "lds_path")):
             durs.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     dur_ns = sum(sum(v) / len(v) for v in durs.values())  # per launch (all its dispatches)
     v["kernel_ns_profiled"] = dur_ns
