@@ -20,7 +20,7 @@ LEGACY_SRCS := $(CSRC)/legacy/convEncode.c $(CSRC)/legacy/convHelpers.c $(CSRC)/
 LEGACY_HDRS := include/viterbiDecoder.h include/viterbiDecoderButterflyk1.h include/convEncode.h include/convHelpers.h
 LEGACY_CFLAGS := -O2 -std=gnu11 -fPIC -Wall -Wno-unused-function -pthread
 
-LEGACY_KS := 3 5 7 9 4_k2n3 3_k3n4 7n3 5n4 9n3 8n3
+LEGACY_KS := 3 5 7 9 4_k2n3 3_k3n4 7n3 5n4 9n3 8n3 3s 4 6 8
 
 .PHONY: all lib legacy oracle testprogs clean
 all: lib legacy oracle testprogs

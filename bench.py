@@ -107,6 +107,29 @@ def free_port():
         return s.getsockname()[1]
 
 
+def debug_bits_dropped(environ):
+    """True (with a message) when $VTB_DEBUG asks for phase-timing bits the loaded library does
+    not honour: the shipped build masks the output-corrupting bits 0-4 (vtb_internal.h
+    kDbgUnsafe), so a phase-timing script run without VTB_LIB_PATH pointing at a -DVTB_MEASURE
+    build (tools/build_variants.sh) would time the full kernel and report it as a phase."""
+    want = environ.get("VTB_DEBUG", "")
+    if not want:
+        return False
+    from convolutionalencdec_amd import native
+
+    try:
+        req = int(want)
+    except ValueError:
+        req = 0
+    got = native.effective_debug_flags()
+    if got == req:
+        return False
+    print(f"bench.py: VTB_DEBUG={req} but the loaded library ({native.LIB_PATH}) honours {got}: the "
+          "phase-timing bits 0-4 need a -DVTB_MEASURE build (tools/build_variants.sh, VTB_LIB_PATH)",
+          file=sys.stderr, flush=True)
+    return True
+
+
 def launch_plan(args, environ, argv, port=None):
     """What this invocation does, decided before any HIP call:
     {"mode": "run" | "spawn" | "error", "world": N, "reason": ..., "cmd": [...] (spawn)}."""
@@ -576,6 +599,8 @@ def main():
         # torchrun's children so that it can tear them down); our exit status is theirs
         print(f"bench.py: {plan['reason']}", file=sys.stderr, flush=True)
         return subprocess.call(plan["cmd"])
+    if debug_bits_dropped(os.environ):
+        return 2
     if args.source == "gpu0":
         return peer_bench(args)
     world, rank, local = dist_env()

@@ -208,6 +208,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
         if (!workspace(vtb::k9_workspace_bytes(a))) return VTB_ERR_NOMEM;
         e = vtb::launch_k9(a);
     } else if (want_lds && vtb::lds_path_supported(a)) {
+        if (vtb::lds_path_global(a) && !workspace(vtb::lds_path_workspace_bytes(a))) return VTB_ERR_NOMEM;
         e = vtb::launch_lds_path(a);
     } else {
         return VTB_ERR_UNSUPPORTED;
@@ -1222,6 +1223,22 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
 int vtb_decode_frame_legacy(const vtb_code_t* code, const uint8_t* coded, int32_t segments, uint8_t* out) {
     if (!code || !coded || !out) return VTB_ERR_INVALID;
     int e = check_code(code);
+    if (e == VTB_ERR_CODE) {
+        // A generator without both end taps: the reference's butterfly still decodes it (the
+        // caller skipped viterbiConfigCheck) with ē = n − e whatever the taps
+        // (viterbiDecoderButterflyk1.c:101-152), which is not the code's Hamming metric.  That
+        // arithmetic, uint8 wrap and renormalisation included, is the general-k kernel's
+        // VTB_GENK_K1_REFERENCE_U8 mode.
+        vtb_genk_code_t gc;
+        std::memset(&gc, 0, sizeof(gc));
+        gc.input_bits = 1;
+        gc.constraint_length = code->constraint_length;
+        gc.coded_bits = 2;
+        gc.flags = VTB_GENK_K1_REFERENCE_U8;
+        gc.generators[0] = code->generators[0];
+        gc.generators[1] = code->generators[1];
+        return vtb_genk_decode_frame_legacy(&gc, coded, segments, out);
+    }
     if (e != VTB_OK) return e;
     const int32_t L = segments - (code->constraint_length - 1);
     if (L < 1) return VTB_ERR_INVALID;

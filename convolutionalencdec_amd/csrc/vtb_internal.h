@@ -7,6 +7,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "viterbi_amd.h"
+
 namespace vtb {
 
 constexpr int kMaxS = 8;  // K <= 9
@@ -74,12 +76,14 @@ void set_debug_tstamp(unsigned long long* p);
 //   checkpoints never match, 17 forced completeness guards (every traceback chain with a block not
 //   known from the frame end skips its checks and re-walks and takes the guard's exact slow
 //   path), 18 K=9 frames on the pair kernel (two frames per wave) where one frame per wave (k9s)
-//   would run.
+//   would run, 19 the generic kernel's global-survivor variant (vtb_lds_path.hip GS) for every
+//   frame length.
 // Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
 //   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE
 //   build (tools/build_variants.sh) honours them; the shipped library masks them off.
 constexpr int kDbgUnsafe = 0x1F;
 constexpr int kDbgTbCap = 1 << 17;
+constexpr int kDbgGenericGs = 1 << 19;
 #ifdef VTB_MEASURE
 constexpr int kDbgHonoured = ~0;
 #else
@@ -89,17 +93,24 @@ constexpr int kDbgHonoured = ~kDbgUnsafe;
 // $VTB_KERNEL: force one kernel family (testing and A/B measurement).
 enum class Force { Any, K7, Gws, K9, Lds, Seg, K7s, Genk, Unknown };
 
+// Each numeric knob: unset, empty or not above its "off" value means the library's own choice
+// (the value production runs with); knobs only ever select exact alternatives or measurement
+// setups.  (Round 5 moved every variable here; the older per-launch readers gave VTB_SEG9_XCD < 0,
+// VTB_SEG_WARM=0 and VTB_SPLIT_WARM=0 other meanings -- those are gone, listed per knob.)
 struct Knobs {
     int dbg = 0;              // $VTB_DEBUG & kDbgHonoured
     Force force = Force::Any;
-    int split_warm = 0;       // $VTB_SPLIT_WARM: fixed split warm-up (0: chosen by occupancy)
-    int genk_warm = -1;       // $VTB_GENK_WARM (-1: 96)
-    int seg_waves = 0;        // $VTB_SEG_WAVES (0: 8, or 4 where 8 do not fit)
-    int seg_warm = 0;         // $VTB_SEG_WARM (0: kSegWarm; set: no adaptive short warm-up)
+    int split_warm = 0;       // $VTB_SPLIT_WARM > 0: fixed split warm-up (rounded down to 48); else chosen by
+                              //   occupancy (0 no longer turns the split kernel off: VTB_DEBUG bit 12 does)
+    int genk_warm = -1;       // $VTB_GENK_WARM >= 0: general-k traceback warm-up; else 96
+    int seg_waves = 0;        // $VTB_SEG_WAVES > 0: SEG kernel waves; else 8, or 4 where 8 do not fit
+    int seg_warm = 0;         // $VTB_SEG_WARM > 0: fixed SEG warm-up and no adaptive short warm-up; else
+                              //   kSegWarm with the adaptive short warm-up (VTB_SEG_ADAPT=0 turns that off)
     bool seg_adapt = true;    // $VTB_SEG_ADAPT != "0"
-    int seg9_wgs = 0;         // $VTB_SEG9_WGS (0: kSeg9Wgs)
-    int seg9_waves = 0;       // $VTB_SEG9_WAVES (0: kSeg9Waves)
-    int seg9_xcd = -1;        // $VTB_SEG9_XCD (-1: automatic)
+    int seg9_wgs = 0;         // $VTB_SEG9_WGS > 0: K=9 SEG workgroups; else kSeg9Wgs
+    int seg9_waves = 0;       // $VTB_SEG9_WAVES > 0: K=9 SEG waves per workgroup; else kSeg9Waves
+    int seg9_xcd = -1;        // $VTB_SEG9_XCD == 0: K=9 SEG grid stride 1 (workgroups spread over the
+                              //   XCDs); any other value or unset: stride 8 (one XCD, one L2)
 };
 Knobs read_knobs();
 
@@ -122,7 +133,13 @@ int current_device_cus();
 
 // Kernel families.  Each returns hipSuccess or the launch error; VTB_ERR_UNSUPPORTED-style
 // shape limits are reported through *_supported() beforehand.
+//
+// The generic kernel (vtb_lds_path.hip), every K and every frame up to VTB_MAX_FRAME_BITS:
+// survivors in LDS while a wave's survivors and input fit one CU's LDS, else (lds_path_global)
+// in a workspace of lds_path_workspace_bytes(a) bytes at Launch::ws (0 when the LDS variant runs).
 bool lds_path_supported(const Launch& a);
+bool lds_path_global(const Launch& a);
+size_t lds_path_workspace_bytes(const Launch& a);
 hipError_t launch_lds_path(const Launch& a);
 
 // K=7, survivors in LDS (vtb_k7_lds.hip): the fast path.

@@ -1398,7 +1398,9 @@ __device__ __forceinline__ void k7_pair(const uint8_t* __restrict__ in, size_t i
             }
         }
         // an unsplit frame with an unproven block: lane 32f walks frame f whole
-        if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) tb_serial_frame<SOFT, GS>(ob, Tpad, cb0, hyb, tg, lds_off, gbase);
+        // (f = 1 without a real frame B decodes a copy of A that is never written out: not walked)
+        if (blk == 0 && (f == 0 || has_b) && uint32_t(unproven >> (32 * f)) != 0)
+            tb_serial_frame<SOFT, GS>(ob, Tpad, cb0, hyb, tg, lds_off, gbase);
     }
     __syncthreads();
     tstamp(table, 2);

@@ -394,7 +394,7 @@ __device__ void stream_traceback9(const StreamArgs& sa, uint8_t* out, size_t out
                 fixed = true;
             }
         }
-        if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) {
+        if (blk == 0 && real && uint32_t(unproven >> (32 * f)) != 0) {  // (no stream B: nothing to walk)
             note_guard(hits);
             uint32_t l = kloc;
             for (int tlo = hi - 48; tlo >= e0; tlo -= 48) put_bits48_global(ob + ((tlo - e0) >> 3), tb48(tlo, l));
@@ -861,7 +861,7 @@ __device__ __forceinline__ void k9_pair(const uint8_t* __restrict__ in, size_t i
             fixed = true;
         }
     }
-    if (blk == 0 && uint32_t(unproven >> (32 * f)) != 0) {
+    if (blk == 0 && (f == 0 || has_b) && uint32_t(unproven >> (32 * f)) != 0) {  // (a lone last frame: no B)
         note_guard(hits);
         uint32_t l = 0;
         for (int tlo = Tpad - 48; tlo >= 0; tlo -= 48) put_bits48(ob, tlo, tb48(cb0 + kColBytes * (tlo >> 4), l));

@@ -56,7 +56,12 @@ class ConvCode:
 
 
 class ViterbiDecoder:
-    """A decode plan: one code, one input format, one frame length, one device."""
+    """A decode plan: one code, one input format, one frame length, one device.
+
+    The testing / measurement switches ($VTB_KERNEL, $VTB_DEBUG, $VTB_SPLIT_WARM, $VTB_SEG_*;
+    csrc/vtb_internal.h Knobs) are read once, when the plan is created: setting them afterwards
+    does not change an existing plan (make a new ViterbiDecoder).  GenKDecoder, which has no plan
+    in the C ABI, reads them on every call."""
 
     def __init__(self, code=ConvCode(), frame_bits=1024, soft=False, device=0):
         self.code = code if isinstance(code, ConvCode) else ConvCode(*code)

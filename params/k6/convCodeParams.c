@@ -1,0 +1,4 @@
+#include "convCodeParams.h"
+
+/* K=6 rate-1/2 generators (octal Proakis convention, MSB = newest input); both generators tap both ends. */
+const uint64_t g[n] = {053, 075};

@@ -224,6 +224,28 @@ def golden_sets(K):
         yield key, L, z[key + "_uncoded"], z[key + "_rx"], z[key + "_decoded"]
 
 
+# tests/golden/lengths.npz (make_golden_lengths.py): reference-decoded frames of every k = 1 rate-1/2
+# constraint length the legacy drop-in builds (params/<name>, oracle/_ref/libref_<name>.so) at
+# L in LENGTHS, BSC p in {0.03, 0.5}.  "k3" is handTraced's non-symmetric code.
+LENGTH_CODES = {"k3": (3, (0b111, 0b110)), "k3s": (3, (0o7, 0o5)), "k4": (4, (0o15, 0o17)), "k5": (5, (0o23, 0o35)),
+                "k6": (6, (0o53, 0o75)), "k7": (7, (0o113, 0o171)), "k8": (8, (0o247, 0o371)),
+                "k9": (9, (0o561, 0o753))}
+LENGTHS = (1, 7, 100, 1001, 4095, 9000, 16383, 16384)
+
+
+def length_sets(names=None, lengths=None):
+    """Yield (key, name, K, g, L, uncoded, rx, decoded) from tests/golden/lengths.npz."""
+    z = load_golden("lengths.npz")
+    sets = manifest()["lengths"]["sets"]
+    for key in sorted(sets, key=lambda k: (k.split("_")[0], sets[k]["L"], sets[k]["p"])):
+        name = key.split("_")[0]
+        info = sets[key]
+        if (names is not None and name not in names) or (lengths is not None and info["L"] not in lengths):
+            continue
+        yield (key, name, info["K"], tuple(info["g"]), info["L"], z[key + "_uncoded"], z[key + "_rx"],
+               z[key + "_decoded"])
+
+
 def random_frames(orc, K, L, frames, p, seed, soft=False, sigma=None, g=None):
     """Seeded terminated frames through a BSC (hard) or BPSK-AWGN + 8-bit quantiser (soft).
 

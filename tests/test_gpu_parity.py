@@ -29,8 +29,18 @@ class Kern(str):
     def need(self, K):
         assert K in KS_OF.get(str(self), (K,)), (self, K)  # (combinations are generated valid)
 
+    def ran(self):
+        """The last decode ran the forced family (plans capture VTB_KERNEL at creation: a stale
+        plan would otherwise pass on another kernel)."""
+        want = FAMILY_INSTANCES.get(str(self))
+        if want:
+            assert native.last_kernel() in want, (str(self), native.last_kernel())
+
 
 KS_OF = {"k7": (7,), "gws": (7,), "k7s": (7,), "k9": (9,), "k9p": (9,)}  # kernel families tied to one K
+# the kernel instances (vtb_debug_last_kernel) each forced family may run
+FAMILY_INSTANCES = {"k7": ("k7_lds", "k7_lds_loop", "k7_lds_split"), "gws": ("k7_global", "k7_global_loop"),
+                    "k9": ("k9", "k9_loop", "k9s"), "k9p": ("k9", "k9_loop"), "lds": ("lds_path", "lds_path_gs")}
 
 
 K9_PAIR = 1 << 18
@@ -82,6 +92,7 @@ def test_hard_golden_vectors(K, kernel):
         d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L)
         assert (d.decode_host(rx) == dec).all(), (K, key)
         assert (dev_decode(d, rx) == dec).all(), (K, key)
+        kernel.ran()
 
 
 @pytest.mark.parametrize("K,kernel", kk([5, 7, 9]), indirect=["kernel"])
@@ -93,19 +104,24 @@ def test_soft_bridge_golden_vectors(K, kernel):
         assert (dev_decode(d, hard_to_soft(rx)) == dec).all(), (K, key)
 
 
-@pytest.mark.parametrize("K,g,kernel", [(K, g, k) for K, g in [(3, (0b111, 0b101)), (5, CODES[5]), (7, CODES[7]),
+@pytest.mark.parametrize("K,g,kernel", [(K, g, k) for K, g in [(3, (0b111, 0b101)), (4, (0o15, 0o17)), (5, CODES[5]),
+                                                              (6, (0o53, 0o75)), (7, CODES[7]), (8, (0o247, 0o371)),
                                                               (9, CODES[9])] for k in kernels_for(K)],
                          indirect=["kernel"])
-@pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000])
+@pytest.mark.parametrize("L", [1, 7, 100, 1001, 2048, 4096, 9000, 16383, 16384])
 def test_hard_random_vs_oracle(orc, K, g, L, kernel):
+    """Every k = 1 rate-1/2 constraint length at every frame length up to VTB_MAX_FRAME_BITS
+    (the reference's MAX_PKT_LEN_UNCODED_BITS, viterbiDecoder.h:18) on every kernel family that
+    decodes it; the generic kernel's GS variant takes the frames its LDS variant cannot hold."""
     kernel.need(K)
-    if L > 4096 and K not in (5, 7) and (kernel == "lds" or K != 9):
-        pytest.skip("survivor memory of this K and L exceeds one CU's LDS (DESIGN.md, frame-length limits)")
+    if kernel == "k7" and L > 9000:
+        pytest.skip("the forced K=7 LDS-resident kernel holds frames up to its LDS capacity (DESIGN.md 4.5)")
     for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
         unc, rx = random_frames(orc, K, L, 257, p, seed + L, g=g)
         expect = orc.decode(K, g, rx, L)
         got = ViterbiDecoder(ConvCode(K, g), frame_bits=L).decode_host(rx)
         assert (got == expect).all(), (K, L, p)
+        kernel.ran()
         if p == 0.0:
             assert (got == unc).all()
 
@@ -119,6 +135,7 @@ def test_soft_random_vs_oracle(orc, K, L, kernel):
         expect = orc.decode(K, CODES[K], q, L, soft=True)
         got = dev_decode(ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=True), q)
         assert (got == expect).all(), (K, L, sigma)
+        kernel.ran()
 
 
 @pytest.mark.parametrize("soft", [False, True])
@@ -191,8 +208,6 @@ def test_k7_long_frames_vs_oracle(orc, L, soft, kernel):
     (VTB_MAX_FRAME_BITS, reference viterbiDecoder.h:18): the global-survivor variant."""
     K = 7
     kernel.need(K)
-    if kernel == "lds" and soft and L == 16384:
-        pytest.skip("survivors of this frame length exceed one CU's LDS for the generic kernel")
     if soft:
         unc, x = random_frames(orc, K, L, 67, 0.0, 31 + L, soft=True, sigma=0.6287)
     else:
@@ -208,8 +223,6 @@ def test_k9_long_frames_vs_oracle(orc, L, soft, kernel):
     """K=9 frames up to the API maximum (reference viterbiDecoder.h:18), odd and even T."""
     K = 9
     kernel.need(K)
-    if kernel == "lds" and L > 4096:
-        pytest.skip("survivors of this frame length exceed one CU's LDS for the generic kernel")
     if soft:
         unc, x = random_frames(orc, K, L, 33, 0.0, 41 + L, soft=True, sigma=0.6287)
     else:

@@ -35,6 +35,7 @@ CAP = 1 << 17       # VTB_DEBUG: every verified chain takes the completeness gua
 NO_SPLIT = 1 << 8   # VTB_DEBUG: never split frames across the halves of a wave
 SEG_OFF = 1 << 10   # VTB_DEBUG: no single-frame SEG kernel
 K9_PAIR = 1 << 18   # VTB_DEBUG: K=9 frames on the pair kernel (not one frame per wave)
+GEN_GS = 1 << 19    # VTB_DEBUG: the generic kernel's global-survivor variant at every length
 
 
 @pytest.fixture(scope="module")
@@ -87,7 +88,12 @@ def _check(counter, got, want, capped, what, reachable=True):
         assert hits == 0, f"{what}: the guard fired {hits} times at the shipped round caps (a cap is too small)"
     elif reachable:
         assert hits > 0, f"{what}: the capped verification never left a chain unproven (test does not exercise the guard)"
+    return hits
 
+
+# kernel instances whose completeness guard counts once per frame (the K=7 pair kernels count once
+# per wave)
+PER_FRAME_GUARD = ("k9", "k9_loop", "k9s", "lds_path", "lds_path_gs")
 
 # (id, K, L, frames, soft, extra VTB_DEBUG bits, VTB_KERNEL, expected kernel instance)
 FRAME_CASES = [
@@ -109,6 +115,10 @@ FRAME_CASES = [
     ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
     ("lds_path_k5", 5, 512, 64, False, 0, None, "lds_path"),
     ("lds_path_k7_soft", 7, 700, 16, True, 0, "lds", "lds_path"),
+    ("lds_path_gs_k5", 5, 16384, 9, False, 0, None, "lds_path_gs"),
+    ("lds_path_gs_k5_soft", 5, 3000, 17, True, GEN_GS, None, "lds_path_gs"),
+    ("lds_path_gs_k7_soft", 7, 2000, 16, True, GEN_GS, "lds", "lds_path_gs"),
+    ("lds_path_gs_k9", 9, 1500, 5, False, GEN_GS, "lds", "lds_path_gs"),
 ]
 
 
@@ -122,7 +132,11 @@ def test_frame_kernels(orc, counter, monkeypatch, case, capped):
     d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
     got = d.decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
     assert native.last_kernel() == inst, native.last_kernel()
-    _check(counter, got, want, capped, name)
+    hits = _check(counter, got, want, capped, name)
+    if capped and inst in PER_FRAME_GUARD:
+        # one count per real frame: every frame here has blocks not known from its end, and a
+        # lone last frame of a pair kernel has no frame B to walk (odd F counted F + 1)
+        assert hits == F, (name, hits, F)
 
 
 @pytest.mark.parametrize("capped", [True, False], ids=["forced", "shipped"])

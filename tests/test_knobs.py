@@ -77,3 +77,20 @@ def test_unsafe_mask_constant():
     assert "constexpr int kDbgUnsafe = 0x1F;" in src
     assert re.search(r"#ifdef VTB_MEASURE\s+constexpr int kDbgHonoured = ~0;\s+#else\s+constexpr int kDbgHonoured = "
                      r"~kDbgUnsafe;\s+#endif", src)
+
+
+def test_every_knob_documents_its_default():
+    """Each environment knob read_knobs parses is documented in vtb_internal.h's Knobs with the
+    meaning of an unset (or off) value (knob meanings changed silently once)."""
+    api = open(os.path.join(CSRC, "vtb_api.hip")).read()
+    body = api[api.index("Knobs read_knobs() {"):]
+    body = body[:body.index("\n}\n")]
+    names = set(re.findall(r'"(VTB_[A-Z0-9_]+)"', body))
+    hdr = open(os.path.join(CSRC, "vtb_internal.h")).read()
+    knobs = hdr[hdr.index("struct Knobs {"):]
+    knobs = knobs[:knobs.index("};")]
+    for name in names - {"VTB_DEBUG", "VTB_KERNEL"}:
+        i = knobs.find("$" + name)
+        assert i >= 0, f"{name} is not documented in Knobs"
+        doc = knobs[i:i + 200]
+        assert "else" in doc or "unset" in doc or "!=" in doc, f"{name}: no default meaning documented"
