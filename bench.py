@@ -46,7 +46,9 @@ sys.path.insert(0, REPO)
 METRIC = "decoded info Mbit/s, K=7 r=1/2 soft-dec, batch 4096 frames @1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 K, G = 7, (0o113, 0o171)
-CODES = {5: (5, (0o23, 0o35)), 7: (7, G), 9: (9, (0o561, 0o753))}
+# every k = 1 rate-1/2 constraint length (K = 3, 4, 6, 8: the generic kernel; params/k<K>)
+CODES = {3: (3, (0o7, 0o5)), 4: (4, (0o15, 0o17)), 5: (5, (0o23, 0o35)), 6: (6, (0o53, 0o75)), 7: (7, G),
+         8: (8, (0o247, 0o371)), 9: (9, (0o561, 0o753))}
 
 
 def parse(argv=None):
@@ -57,7 +59,7 @@ def parse(argv=None):
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU")
     ap.add_argument("--frame-bits", type=int, default=1024)
     ap.add_argument("--hard", action="store_true", help="hard-decision input instead of 8-bit soft")
-    ap.add_argument("--K", type=int, default=7, choices=(5, 7, 9))
+    ap.add_argument("--K", type=int, default=7, choices=tuple(range(3, 10)))
     ap.add_argument("--snr-db", type=float, default=-5.0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,

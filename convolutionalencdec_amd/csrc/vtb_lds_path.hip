@@ -12,9 +12,9 @@
 // This is the simple, obviously-correct kernel: the register-resident kernel
 // (vtb_k7_lds.hip) is the fast path; this one also covers every K in 3..9.
 //
-// Two variants of the one kernel (template parameter GS):
+// Two variants of the one kernel (template parameter GS; lds_path_global picks one):
 //   * LDS: every survivor word and the wave's whole input in LDS, 8 R T + F T B bytes per wave
-//     (B = 1 hard, 2 soft) -- short frames;
+//     (B = 1 hard, 2 soft) -- K = 3, 4 while that LDS leaves the CU the batch's waves;
 //   * GS (global survivors): the survivor words in a global workspace (8 R T bytes per wave,
 //     the lane that owns step t mod 64 keeps its ballot words in registers and the wave stores
 //     64 steps' words at once, coalesced), the input staged through LDS kStage steps at a time
@@ -192,18 +192,47 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     // The state after step t is s; its bit 0 is the information bit of step t, and the
     // predecessor is (s >> 1) | (decision << (S - 1)).
     constexpr int kWarm = 8 * S + 48;
-    auto pred = [&](unsigned st, int t) -> unsigned {
-        const uint64_t w = dec[(size_t)t * R + (st / G)];
-        return (st >> 1) | (unsigned((w >> (fi * G + (st % G))) & 1u) << (S - 1));
+    // A step's R survivor words do not depend on the walk's state (only the bit taken from them
+    // does), so the walks load kTb steps' words at once and then take the kTb dependent steps:
+    // kTb loads in flight instead of one (GS: L2 / HBM latency; LDS: ds_read latency).
+    constexpr int kTb = R == 4 ? 4 : 8;
+    auto row = [&](int t, uint64_t (&w)[R]) {
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r] = dec[(size_t)t * R + r];
+    };
+    auto step = [&](unsigned st, const uint64_t (&w)[R]) -> unsigned {
+        uint64_t x = w[0];
+        if constexpr (R == 2) x = (st & unsigned(G)) ? w[1] : w[0];
+        if constexpr (R == 4) {
+            const uint64_t lo2 = (st & unsigned(G)) ? w[1] : w[0], hi2 = (st & unsigned(G)) ? w[3] : w[2];
+            x = (st & unsigned(2 * G)) ? hi2 : lo2;
+        }
+        return (st >> 1) | (unsigned((x >> (fi * G + (st % G))) & 1u) << (S - 1));
+    };
+    // the state before steps [lo, hi) given the state after step hi - 1
+    auto walk = [&](unsigned st, int hi, int lo) -> unsigned {
+        int t = hi;
+        for (; t - kTb >= lo; t -= kTb) {
+            uint64_t w[kTb][R];
+#pragma unroll
+            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
+#pragma unroll
+            for (int j = 0; j < kTb; j++) st = step(st, w[j]);
+        }
+        for (; t > lo; t--) {
+            uint64_t w[R];
+            row(t - 1, w);
+            st = step(st, w);
+        }
+        return st;
     };
     const int tbb = ((T + G - 1) / G + 7) / 8 * 8;
     const int lo = lam * tbb, top = lo + tbb < T ? lo + tbb : T;
     const bool active = lo < T;
     const int start = top + kWarm < T ? top + kWarm : T;
-    unsigned st = 0;
-    for (int t = start - 1; active && t >= top; t--) st = pred(st, t);
+    unsigned st = active ? walk(0u, start, top) : 0u;
     unsigned s_top = st;
-    for (int t = top - 1; active && t >= lo; t--) st = pred(st, t);
+    if (active) st = walk(st, top, lo);
     unsigned fin = st;
     bool fixed = !active || start == T;
     const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
@@ -224,9 +253,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         }
         const uint64_t badf = (bad & fmask) >> (fi * G);  // this frame's failed blocks
         if (!ok && (badf >> (lam + 1)) == 0) {
-            st = s_top = sf;
-            for (int t = top - 1; t >= lo; t--) st = pred(st, t);
-            fin = st;
+            s_top = sf;
+            fin = walk(sf, top, lo);
             fixed = true;
         }
     }
@@ -237,13 +265,34 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         if (lam == 0 && valid) note_guard(table.guard_hits);
     }
     if (!valid || !emit) return;
+    // Emission, MSB-first bytes (reference :243-249): bit t of the frame is bit 0 of the state
+    // after step t; byte t / 8 is complete at step t = 0 mod 8 (elo is a multiple of 8).  The
+    // steps above the last whole octet of [elo, etop) one by one, then octets with their 8 rows
+    // loaded at once.
     uint8_t* o = out + myframe * out_stride;
     unsigned byte = 0;
     st = s_top;
-    for (int t = etop - 1; t >= elo; t--) {
+    auto put = [&](int t) {
+        if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
+    };
+    int t = etop - 1;
+    for (; t >= elo && ((t + 1) & 7) != 0; t--) {
         byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
-        if ((t & 7) == 0 && t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
-        st = pred(st, t);
+        if ((t & 7) == 0) put(t);
+        uint64_t w[R];
+        row(t, w);
+        st = step(st, w);
+    }
+    for (; t >= elo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
+        uint64_t w[8][R];
+#pragma unroll
+        for (int j = 0; j < 8; j++) row(t - j, w[j]);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
+            st = step(st, w[j]);
+        }
+        put(t - 7);
     }
 }
 
@@ -341,10 +390,26 @@ bool lds_path_supported(const Launch& a) {
     return a.S >= 2 && a.S <= kMaxS && a.T > a.S && a.T <= VTB_MAX_FRAME_BITS + a.S;
 }
 
+// Which variant runs (measured on MI355X, 4,096-frame batches, K = 3..8 x L = 1,024..16,384,
+// tools/generic_sweep.py, profiles/r06/generic/sweep.jsonl):
+//  * S >= 4 (16+ lanes per frame): GS always -- its traceback blocks are short (T / G steps per
+//    lane), and with a few KB of LDS per wave the CU holds every wave the batch gives it; it ran
+//    0-4 % faster than the LDS variant where both fit (K = 5, 6 at L = 1,024) and 2-10x faster
+//    where the LDS variant's survivors cut the waves per CU (K = 5, L = 4,096: 34.5 against 18.7
+//    Gbit/s; K = 8, L = 4,096: 17.8 against 3.7);
+//  * S <= 3 (4 or 8 lanes per frame, 16 or 8 frames per wave): the LDS variant while its
+//    survivors leave the CU the waves the batch needs (K = 3, L = 4,096, one wave per CU: 24.3
+//    against 20.8 Gbit/s -- a lane walks T / 4 steps, from LDS rather than L2), else GS (K = 4 soft,
+//    L = 4,096: 23.2 against 13.2).
 bool lds_path_global(const Launch& a) {
     if (a.dbg & kDbgGenericGs) return true;
+    if (a.S >= 4) return true;
     const size_t w = bytes_per_wave(a.S, a.soft, a.T);
-    return w == 0 || w > kLdsLimit;
+    if (w == 0 || w > kLdsLimit) return true;
+    const size_t cus = a.cus > 0 ? (size_t)a.cus : 256;
+    size_t need = (gs_waves(a) + cus - 1) / cus;  // waves per CU the batch gives
+    if (need > 8) need = 8;
+    return kLdsLimit / w < need;
 }
 
 size_t lds_path_workspace_bytes(const Launch& a) {

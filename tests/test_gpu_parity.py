@@ -115,7 +115,13 @@ def test_hard_random_vs_oracle(orc, K, g, L, kernel):
     decodes it; the generic kernel's GS variant takes the frames its LDS variant cannot hold."""
     kernel.need(K)
     if kernel == "k7" and L > 9000:
-        pytest.skip("the forced K=7 LDS-resident kernel holds frames up to its LDS capacity (DESIGN.md 4.5)")
+        # the forced K=7 LDS-resident kernel holds frames up to its LDS capacity (DESIGN.md 4.5):
+        # refused with an error code, never a wrong result (the library's own choice takes them)
+        unc, rx = random_frames(orc, K, L, 3, 0.06, 12 + L, g=g)
+        with pytest.raises(native.VtbError) as e:
+            ViterbiDecoder(ConvCode(K, g), frame_bits=L).decode_host(rx)
+        assert e.value.code == native.VTB_ERR_UNSUPPORTED
+        return
     for p, seed in ((0.0, 11), (0.06, 12), (0.5, 13)):
         unc, rx = random_frames(orc, K, L, 257, p, seed + L, g=g)
         expect = orc.decode(K, g, rx, L)

@@ -36,6 +36,7 @@ NO_SPLIT = 1 << 8   # VTB_DEBUG: never split frames across the halves of a wave
 SEG_OFF = 1 << 10   # VTB_DEBUG: no single-frame SEG kernel
 K9_PAIR = 1 << 18   # VTB_DEBUG: K=9 frames on the pair kernel (not one frame per wave)
 GEN_GS = 1 << 19    # VTB_DEBUG: the generic kernel's global-survivor variant at every length
+GUARD_CODES = {**CODES, 3: (0o7, 0o5), 4: (0o15, 0o17)}
 
 
 @pytest.fixture(scope="module")
@@ -58,16 +59,16 @@ def counter():
     native.set_guard_counter(0)
 
 
-def _noisy(orc, K, L, F, soft, seed):
+def _noisy(orc, K, L, F, soft, seed, g=None):
     """Half pure-noise frames (paths do not merge within the walk warm-up), half at moderate
     noise (some blocks verify in the first round, others need re-walks)."""
     h = F // 2
     if soft:
-        _, a = random_frames(orc, K, L, h, 0.0, seed, soft=True, sigma=4.0)
-        _, b = random_frames(orc, K, L, F - h, 0.0, seed + 1, soft=True, sigma=0.9)
+        _, a = random_frames(orc, K, L, h, 0.0, seed, soft=True, sigma=4.0, g=g)
+        _, b = random_frames(orc, K, L, F - h, 0.0, seed + 1, soft=True, sigma=0.9, g=g)
     else:
-        _, a = random_frames(orc, K, L, h, 0.5, seed)
-        _, b = random_frames(orc, K, L, F - h, 0.09, seed + 1)
+        _, a = random_frames(orc, K, L, h, 0.5, seed, g=g)
+        _, b = random_frames(orc, K, L, F - h, 0.09, seed + 1, g=g)
     return np.ascontiguousarray(np.concatenate([a, b]).reshape(F, -1))
 
 
@@ -113,9 +114,10 @@ FRAME_CASES = [
     ("k9_soft", 9, 1024, 64, True, K9_PAIR, None, "k9"),
     ("k9_hard", 9, 1001, 33, False, K9_PAIR, None, "k9"),
     ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
-    ("lds_path_k5", 5, 512, 64, False, 0, None, "lds_path"),
-    ("lds_path_k7_soft", 7, 700, 16, True, 0, "lds", "lds_path"),
+    ("lds_path_k3", 3, 512, 64, False, 0, None, "lds_path"),
+    ("lds_path_k4_soft", 4, 700, 16, True, 0, None, "lds_path"),
     ("lds_path_gs_k5", 5, 16384, 9, False, 0, None, "lds_path_gs"),
+    ("lds_path_gs_k3", 3, 9000, 40, False, 0, None, "lds_path_gs"),
     ("lds_path_gs_k5_soft", 5, 3000, 17, True, GEN_GS, None, "lds_path_gs"),
     ("lds_path_gs_k7_soft", 7, 2000, 16, True, GEN_GS, "lds", "lds_path_gs"),
     ("lds_path_gs_k9", 9, 1500, 5, False, GEN_GS, "lds", "lds_path_gs"),
@@ -126,10 +128,11 @@ FRAME_CASES = [
 @pytest.mark.parametrize("case", FRAME_CASES, ids=[c[0] for c in FRAME_CASES])
 def test_frame_kernels(orc, counter, monkeypatch, case, capped):
     name, K, L, F, soft, extra, kernel, inst = case
-    x = _noisy(orc, K, L, F, soft, 700 + K + L)
-    want = orc.decode(K, CODES[K], x, L, soft=soft, threads=16)
+    g = GUARD_CODES[K]
+    x = _noisy(orc, K, L, F, soft, 700 + K + L, g)
+    want = orc.decode(K, g, x, L, soft=soft, threads=16)
     _set_env(monkeypatch, (CAP if capped else 0) | extra, kernel)
-    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
     got = d.decode_device(torch.from_numpy(x).cuda()).cpu().numpy()
     assert native.last_kernel() == inst, native.last_kernel()
     hits = _check(counter, got, want, capped, name)
