@@ -14,7 +14,8 @@
 //
 // Two variants of the one kernel (template parameter GS; lds_path_global picks one):
 //   * LDS: every survivor word and the wave's whole input in LDS, 8 R T + F T B bytes per wave
-//     (B = 1 hard, 2 soft) -- K = 3, 4 while that LDS leaves the CU the batch's waves;
+//     (B = 1 hard, 2 soft) -- K = 3, 4 frames of 2,048+ steps while that LDS leaves the CU
+//     the batch's waves;
 //   * GS (global survivors): the survivor words in a global workspace (8 R T bytes per wave,
 //     the lane that owns step t mod 64 keeps its ballot words in registers and the wave stores
 //     64 steps' words at once, coalesced), the input staged through LDS kStage steps at a time
@@ -200,14 +201,20 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
 #pragma unroll
         for (int r = 0; r < R; r++) w[r] = dec[(size_t)t * R + r];
     };
+    // (each word's bit is taken before the select: a select between the 64-bit words is
+    // compiled as a dynamically indexed array in scratch memory)
     auto step = [&](unsigned st, const uint64_t (&w)[R]) -> unsigned {
-        uint64_t x = w[0];
-        if constexpr (R == 2) x = (st & unsigned(G)) ? w[1] : w[0];
+        const unsigned sh = unsigned(fi * G) + (st % G);
+        unsigned b[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) b[r] = unsigned(w[r] >> sh) & 1u;
+        unsigned x = b[0];
+        if constexpr (R == 2) x = (st & unsigned(G)) ? b[1] : b[0];
         if constexpr (R == 4) {
-            const uint64_t lo2 = (st & unsigned(G)) ? w[1] : w[0], hi2 = (st & unsigned(G)) ? w[3] : w[2];
+            const unsigned lo2 = (st & unsigned(G)) ? b[1] : b[0], hi2 = (st & unsigned(G)) ? b[3] : b[2];
             x = (st & unsigned(2 * G)) ? hi2 : lo2;
         }
-        return (st >> 1) | (unsigned((x >> (fi * G + (st % G))) & 1u) << (S - 1));
+        return (st >> 1) | (x << (S - 1));
     };
     // the state before steps [lo, hi) given the state after step hi - 1
     auto walk = [&](unsigned st, int hi, int lo) -> unsigned {
@@ -391,19 +398,17 @@ bool lds_path_supported(const Launch& a) {
 }
 
 // Which variant runs (measured on MI355X, 4,096-frame batches, K = 3..8 x L = 1,024..16,384,
-// tools/generic_sweep.py, profiles/r06/generic/sweep.jsonl):
-//  * S >= 4 (16+ lanes per frame): GS always -- its traceback blocks are short (T / G steps per
-//    lane), and with a few KB of LDS per wave the CU holds every wave the batch gives it; it ran
-//    0-4 % faster than the LDS variant where both fit (K = 5, 6 at L = 1,024) and 2-10x faster
-//    where the LDS variant's survivors cut the waves per CU (K = 5, L = 4,096: 34.5 against 18.7
-//    Gbit/s; K = 8, L = 4,096: 17.8 against 3.7);
-//  * S <= 3 (4 or 8 lanes per frame, 16 or 8 frames per wave): the LDS variant while its
-//    survivors leave the CU the waves the batch needs (K = 3, L = 4,096, one wave per CU: 24.3
-//    against 20.8 Gbit/s -- a lane walks T / 4 steps, from LDS rather than L2), else GS (K = 4 soft,
-//    L = 4,096: 23.2 against 13.2).
+// tools/generic_sweep.py, profiles/r06/generic/sweep_r06c_batched_walk_noscratch.jsonl): GS, whose
+// waves need a few KB of LDS each (the CU holds every wave the batch gives it) and whose walks
+// load kTb steps' words at once, ran at or above the LDS variant everywhere (K = 4, L = 4,096
+// hard: 35.4 against 34.1 Gbit/s; K = 8, L = 4,096: 18.6 against 3.7, the LDS survivors cutting
+// the CU to one wave) except for K = 3 frames of 2,048+ steps, where a lane's walk covers T / 4
+// steps and the LDS variant fits the one wave per CU a 4,096-frame batch gives (L = 4,096 hard:
+// 27.6 against 26.1).  So: the LDS variant for K <= 4 frames of T >= 2,048 steps while it leaves
+// the CU the waves the batch needs, GS for everything else.
 bool lds_path_global(const Launch& a) {
     if (a.dbg & kDbgGenericGs) return true;
-    if (a.S >= 4) return true;
+    if (a.S >= 4 || a.T < 2048) return true;
     const size_t w = bytes_per_wave(a.S, a.soft, a.T);
     if (w == 0 || w > kLdsLimit) return true;
     const size_t cus = a.cus > 0 ? (size_t)a.cus : 256;

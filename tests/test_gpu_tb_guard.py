@@ -114,8 +114,8 @@ FRAME_CASES = [
     ("k9_soft", 9, 1024, 64, True, K9_PAIR, None, "k9"),
     ("k9_hard", 9, 1001, 33, False, K9_PAIR, None, "k9"),
     ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
-    ("lds_path_k3", 3, 512, 64, False, 0, None, "lds_path"),
-    ("lds_path_k4_soft", 4, 700, 16, True, 0, None, "lds_path"),
+    ("lds_path_k3", 3, 3000, 64, False, 0, None, "lds_path"),
+    ("lds_path_k4_soft", 4, 2500, 16, True, 0, None, "lds_path"),
     ("lds_path_gs_k5", 5, 16384, 9, False, 0, None, "lds_path_gs"),
     ("lds_path_gs_k3", 3, 9000, 40, False, 0, None, "lds_path_gs"),
     ("lds_path_gs_k5_soft", 5, 3000, 17, True, GEN_GS, None, "lds_path_gs"),

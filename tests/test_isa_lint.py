@@ -54,6 +54,11 @@ def test_shipped_kernels_have_no_asm_load_hazard(tmp_path):
     # the lint must have had something to check: the K=7 / K=9 kernels issue asm loads
     for name in ("vtb_k7_lds.hip", "vtb_k9.hip"):
         assert asm_global_loads(asm[name]) > 0, name
+    # no kernel spills to or indexes into scratch memory (round 6: a select between 64-bit
+    # survivor words in the generic traceback compiled to a dynamically indexed scratch array)
+    scratch = {n: sum(1 for ln in s.split("\n") if ln.strip().startswith(("scratch_", "buffer_store", "buffer_load")))
+               for n, s in asm.items()}
+    assert not any(scratch.values()), scratch
 
 
 def asm_global_loads(text):
