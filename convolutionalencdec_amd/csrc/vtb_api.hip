@@ -158,7 +158,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     // K=7: survivors in LDS while that LDS leaves the CU as many waves (2 frames each) as
     // the batch can give it, up to 2 per SIMD (the ACS is VALU-bound there: more waves do
     // not help); else survivors in a global workspace (3 KB LDS per wave, traceback from
-    // L2/HBM).  Measured: 4096 x 1024 soft, LDS 36.4 us vs global 46.3 us;
+    // L2/HBM).  Measured (PERF_LOG.md §4.2): 4096 x 1024 soft, LDS 36.4 us vs global 46.3 us;
     // 65536 x 2048, LDS (1 wave per SIMD) 1.56 ms vs global 0.94 ms.  Other K: the generic
     // LDS-path kernel.
     bool k7_in_lds = false;
@@ -187,7 +187,7 @@ int launch(vtb_plan* p, const uint8_t* d_in, size_t in_stride, uint8_t* d_out, s
     // frame per wave as two halves with LDS survivors, persistent (launch_k7_split_loop), when
     // the halves fit 8 waves per CU.  Halves whose metrics disagree at the seam are fixed up in
     // the wave (k7_pair); only frames the fix-up cannot settle go to the list kernel.  Measured
-    // on C3 shapes (round 3, DESIGN.md §4.2b, 65,536 x 2,048 bits): soft -5 dB 1.019 ms, no
+    // on C3 shapes (round 3, PERF_LOG.md §4.2b, 65,536 x 2,048 bits): soft -5 dB 1.019 ms, no
     // frame to the list (without the fix-up 1.065 ms, 1,528 frames listed); hard p = 0.056
     // 0.808 ms against 0.805 for the global-survivor variant, whose survivor words leave the CU
     // (7.5x the algorithmic HBM bytes).  VTB_KERNEL=k7s forces it wherever it applies;

@@ -100,7 +100,7 @@ constexpr int kTbWarm = 48;  // traceback warm-up steps past a block's end (mult
 constexpr int kPrioPct = 67;
 constexpr uint32_t kR1 = 0x10001u;
 // Soft renormalisation period in steps (divides the 48-step chunk).  16 would overflow the u16
-// metrics on padding rows (tests/test_metric_bounds.py).
+// metrics on padding rows (PERF_LOG.md §5; tests/test_metric_bounds.py).
 constexpr int kRenormSoft = 12;
 
 // History bits per u16 half: soft input keeps 4m + h (2 history bits, the

@@ -1,5 +1,5 @@
-"""GPU: the K=7 split-frame kernels and their in-wave fix-up (DESIGN.md 4.1 "Split frames",
-4.2b "Round 3: the in-wave fix-up"), bit for bit against the oracle.
+"""GPU: the K=7 split-frame kernels and their in-wave fix-up (DESIGN.md 4.1 "Shapes", 4.2b;
+PERF_LOG.md 4.2b "Round 3: the in-wave fix-up"), bit for bit against the oracle.
 
 A split frame is decoded in one wave as two halves: A = steps [0, t1) from the reference's
 start metrics, B = [t1 - warm, T) from equal metrics.  When B's metric vector at t1 is not A's

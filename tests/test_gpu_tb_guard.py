@@ -1,4 +1,4 @@
-"""GPU: the traceback completeness guard of every kernel family (DESIGN.md 4.1 "Traceback",
+"""GPU: the traceback completeness guard of every kernel family (DESIGN.md 4.0 "Traceback rule",
 round-5 item 1).
 
 Every kernel traces back in verified block-parallel chains: a block is proven once it entered on

@@ -14,7 +14,7 @@ bounds are checked here on the arithmetic itself, from the constants in the kern
   W = SC·INIT to the partner candidate, INIT = (K - 1)·n·Q + 1 (vtb_k7_lds.hip stage_write).
 
 Round 4 found that the round-2 argument for a 16-step soft period omitted the padding rows
-(DESIGN.md 5); these tests pin the shipped period and show why 16 does not fit.
+(PERF_LOG.md 5); these tests pin the shipped period and show why 16 does not fit.
 """
 import os
 import re

@@ -1,5 +1,5 @@
 """CPU: a model of the block-parallel traceback's verification loop and its completeness guard
-(DESIGN.md 4.1 "Traceback", 4.2b), checked against the round cap of every loop in the kernels.
+(DESIGN.md 4.0 "Traceback rule", 4.2b), checked against the round cap of every loop in the kernels.
 
 Each lane walks one block of a chain from an unverified start; a block is proven when it entered
 on its successor's exit and every later block is proven (the chain's last block is known).  A
