@@ -1,18 +1,19 @@
 #!/bin/bash
-# Round-5 GPU steps, each under its own time limit, stopping at the first failure.
-#   tools/gpu_r05.sh guard   the completeness-guard tests (tests/test_gpu_tb_guard.py)
-#   tools/gpu_r05.sh suite   the whole GPU suite, smoke() and the driver's bench command
-#   tools/gpu_r05.sh bench   the driver's bench command only (twice)
-#   tools/gpu_r05.sh prof    rocprofv3 kernel trace + stats of the bench command (the library's
+# GPU steps of a round (output under gpurun_out/$ROUND, default r06), each under its own time
+# limit, stopping at the first failure.
+#   tools/gpu_round.sh guard   the completeness-guard tests (tests/test_gpu_tb_guard.py)
+#   tools/gpu_round.sh suite   the whole GPU suite, smoke() and the driver's bench command
+#   tools/gpu_round.sh bench   the driver's bench command only (twice)
+#   tools/gpu_round.sh prof    rocprofv3 kernel trace + stats of the bench command (the library's
 #                            sha beside it for tools/kernel_time_summary.py)
-#   tools/gpu_r05.sh fuzz    one fuzz sweep and one fix-up sweep on this library (2,000 cases per
+#   tools/gpu_round.sh fuzz    one fuzz sweep and one fix-up sweep on this library (2,000 cases per
 #                            family), plus the fuzz sweep again with every traceback verification
 #                            forced to the guards' slow paths (VTB_DEBUG bit 17)
-#   tools/gpu_r05.sh stamps  PMC passes of every config line, the config lines, SQ passes of the
+#   tools/gpu_round.sh stamps  PMC passes of every config line, the config lines, SQ passes of the
 #                            headline (summarised on the CPU: tools/traffic_summary.py, ...)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r05
+O=gpurun_out/${ROUND:-r06}
 mkdir -p $O
 sha=$(sha256sum convolutionalencdec_amd/lib/libviterbi_amd.so | cut -c1-16)
 echo "lib sha16 $sha" | tee $O/lib_sha16.txt

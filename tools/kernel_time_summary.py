@@ -13,7 +13,7 @@ chosen dispatch indices are recorded in the entry.  Without a trace: the stats f
 over every dispatch.
 
 The library stamp is the sha written next to the profile by the run that profiled it
-(<dir>/lib_sha16.txt, tools/gpu_r05.sh prof), not the library present when this script runs;
+(<dir>/lib_sha16.txt, tools/gpu_round.sh prof), not the library present when this script runs;
 the directory must hold exactly one stats file and at most one trace.
 
     python tools/kernel_time_summary.py <dir> <workload_key> [--warmup W --steps K]

@@ -1,6 +1,6 @@
 """Pair a configs.jsonl (tools/configs.sh) with counter stamps taken afterwards on the same library.
 
-tools/gpu_r05.sh runs the PMC passes and the config lines in one GPU call, so the lines print
+tools/gpu_round.sh runs the PMC passes and the config lines in one GPU call, so the lines print
 before profiles/pmc_traffic.json, pmc_valu.json and isa_mix.json hold this library's entries,
 and their `roofline.traffic` / `roofline.secondary` counters read null.  This fills them in
 with bench.py's own code (load_traffic / load_valu / load_isa_mix, secondary_block), from each
