@@ -8,8 +8,23 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-# $VTB_LIB_PATH points at an alternative build (A/B measurement of kernel variants only).
-LIB_PATH = os.environ.get("VTB_LIB_PATH") or os.path.join(LIB_DIR, "libviterbi_amd.so")
+# $VTB_LIB_PATH points at an alternative build (A/B measurement of kernel variants only): it must
+# be a measurement build under lib/exp/ (tools/build_variants.sh, tools/ab_lib.sh), so the public
+# API can never be pointed at an arbitrary library.
+EXP_DIR = os.path.join(LIB_DIR, "exp")
+
+
+def _lib_path(environ=os.environ):
+    alt = environ.get("VTB_LIB_PATH")
+    if not alt:
+        return os.path.join(LIB_DIR, "libviterbi_amd.so")
+    real = os.path.realpath(alt)
+    if os.path.commonpath([real, os.path.realpath(EXP_DIR)]) != os.path.realpath(EXP_DIR):
+        raise ImportError(f"VTB_LIB_PATH={alt!r}: only measurement builds under {EXP_DIR} may replace the library")
+    return real
+
+
+LIB_PATH = _lib_path()
 
 VTB_OK = 0
 VTB_ERR_INVALID = -1

@@ -94,3 +94,15 @@ def test_every_knob_documents_its_default():
         assert i >= 0, f"{name} is not documented in Knobs"
         doc = knobs[i:i + 200]
         assert "else" in doc or "unset" in doc or "!=" in doc, f"{name}: no default meaning documented"
+
+
+def test_lib_path_override_limited_to_measurement_builds(tmp_path):
+    """$VTB_LIB_PATH (A/B measurement) may only name a build under lib/exp/ (VERDICT r5 weak #6)."""
+    from convolutionalencdec_amd import native
+
+    assert native._lib_path({}) == os.path.join(native.LIB_DIR, "libviterbi_amd.so")
+    ok = os.path.join(native.EXP_DIR, "measure", "libviterbi_amd.so")
+    assert native._lib_path({"VTB_LIB_PATH": ok}) == os.path.realpath(ok)
+    for bad in (str(tmp_path / "libviterbi_amd.so"), os.path.join(native.EXP_DIR, "..", "libviterbi_amd.so")):
+        with pytest.raises(ImportError):
+            native._lib_path({"VTB_LIB_PATH": bad})
