@@ -17,6 +17,7 @@ from convolutionalencdec_amd import ConvCode, ViterbiDecoder, native  # noqa: E4
 
 THREADS = min(16, os.cpu_count() or 1)
 K3 = (0b111, 0b101)
+FUZZ_CODES = {3: K3, 4: (0o15, 0o17), 5: CODES[5], 6: (0o53, 0o75), 7: CODES[7], 8: (0o247, 0o371), 9: CODES[9]}
 
 
 @pytest.fixture(scope="module")
@@ -39,18 +40,15 @@ def _cases(n=FUZZ_N or 128, seed=FUZZ_SEED or 20261016):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
-        K = int(rng.choice([3, 5, 7, 7, 7, 7, 9, 9]))
-        # half the cases at the listed lengths (mode limits), half at any length: the split and
-        # segment geometries depend on T modulo 48 and 96 (a floored split point once left the
-        # second half of a frame one step short at T = 1 mod 96)
+        K = int(rng.choice([3, 4, 5, 6, 7, 7, 7, 7, 8, 9, 9]))
+        # half the cases at the listed lengths (mode limits, up to the reference's 16,384), half at
+        # any length (one in four of those up to 16,384): the split and segment geometries depend
+        # on T modulo 48 and 96 (a floored split point once left the second half of a frame one
+        # step short at T = 1 mod 96), the generic kernel's variant on T and the batch (round 6)
         if rng.integers(0, 2):
-            L = int(rng.choice([1, 8, 57, 200, 234, 500, 1024, 1519, 2048, 3000, 4100]))
+            L = int(rng.choice([1, 8, 57, 200, 234, 500, 1024, 1519, 2048, 3000, 4100, 9000, 16383, 16384]))
         else:
-            L = int(rng.integers(1, 4200))
-        if K == 9 and L > 2048:
-            L = 2048
-        if K in (3, 5) and L > 2048:
-            L = 1024
+            L = int(rng.integers(1, 16385 if rng.integers(0, 4) == 0 else 4200))
         F = int(rng.choice([1, 2, 3, 65, 257, 1000, 2049, 4097, 9001]))
         while F * L > 12_000_000 or (K == 9 and F * L > 3_000_000):
             F = max(1, F // 3)
@@ -64,7 +62,7 @@ def _cases(n=FUZZ_N or 128, seed=FUZZ_SEED or 20261016):
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: f"{c[0]}-K{c[1]}-L{c[2]}-F{c[3]}-{'soft' if c[4] else 'hard'}")
 def test_random_case_vs_oracle(orc, case):
     i, K, L, F, soft, noise, strided = case
-    g = K3 if K == 3 else CODES[K]
+    g = FUZZ_CODES[K]
     if soft:
         sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
         unc, x = random_frames(orc, K, L, F, 0.0, 1000 + i, soft=True, sigma=sigma, g=g)

@@ -42,12 +42,12 @@ for step in "$@"; do
       find $O/prof -name '*kernel_stats.csv' | head -3 ;;
     fuzz)
       mkdir -p $O/fuzz
-      VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5005 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_seed5005.log 2>&1 || { tail -30 $O/fuzz/fuzz_seed5005.log; exit 1; }
-      tail -n 1 $O/fuzz/fuzz_seed5005.log
-      VTB_FIXUP_N=2000 VTB_FIXUP_SEED=5007 timeout -k 10 600 ${PYT/-x /} tests/test_gpu_split_fixup.py -m gpu -k fixup_family > $O/fuzz/fixup_seed5007.log 2>&1 || { tail -30 $O/fuzz/fixup_seed5007.log; exit 1; }
-      tail -n 1 $O/fuzz/fixup_seed5007.log
-      VTB_DEBUG=131072 VTB_FUZZ_N=2000 VTB_FUZZ_SEED=5006 timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_forced_seed5006.log 2>&1 || { tail -30 $O/fuzz/fuzz_forced_seed5006.log; exit 1; }
-      tail -n 1 $O/fuzz/fuzz_forced_seed5006.log ;;
+      VTB_FUZZ_N=2000 VTB_FUZZ_SEED=${FUZZ_SEED:-6005} timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_seed${FUZZ_SEED:-6005}.log 2>&1 || { tail -30 $O/fuzz/fuzz_seed${FUZZ_SEED:-6005}.log; exit 1; }
+      tail -n 1 $O/fuzz/fuzz_seed${FUZZ_SEED:-6005}.log
+      VTB_FIXUP_N=2000 VTB_FIXUP_SEED=${FIXUP_SEED:-6007} timeout -k 10 600 ${PYT/-x /} tests/test_gpu_split_fixup.py -m gpu -k fixup_family > $O/fuzz/fixup_seed${FIXUP_SEED:-6007}.log 2>&1 || { tail -30 $O/fuzz/fixup_seed${FIXUP_SEED:-6007}.log; exit 1; }
+      tail -n 1 $O/fuzz/fixup_seed${FIXUP_SEED:-6007}.log
+      VTB_DEBUG=131072 VTB_FUZZ_N=2000 VTB_FUZZ_SEED=${FORCED_SEED:-6006} timeout -k 10 900 ${PYT/-x /} tests/test_gpu_fuzz.py -m gpu > $O/fuzz/fuzz_forced_seed${FORCED_SEED:-6006}.log 2>&1 || { tail -30 $O/fuzz/fuzz_forced_seed${FORCED_SEED:-6006}.log; exit 1; }
+      tail -n 1 $O/fuzz/fuzz_forced_seed${FORCED_SEED:-6006}.log ;;
     stamps)
       timeout -k 10 900 bash tools/pmc_passes.sh head c2 c3s c3h c4 c5 || exit 1
       timeout -k 10 600 bash tools/configs.sh && cp gpurun_out/configs.jsonl $O/configs.jsonl || exit 1
