@@ -333,10 +333,18 @@ int states_per_lane(int S) { return S <= 6 ? 1 : (1 << S) / 64; }
 int frames_per_wave(int S) { return S >= 6 ? 1 : 64 >> S; }
 size_t gs_bytes_per_wave(const Launch& a) { return (size_t)a.T * states_per_lane(a.S) * 8; }
 size_t gs_waves(const Launch& a) { return (a.frames + frames_per_wave(a.S) - 1) / frames_per_wave(a.S); }
+// Waves per launch: at most 1 GiB of survivor words, but never fewer than the CUs hold at once
+// (32 per CU), and the launches of one batch balanced -- a remainder launch of a few waves runs a
+// whole frame's dependent steps at low occupancy (K = 8, 4,096 x 16,384 bits: 4,094 + 2 waves
+// took 5.5 ms against one launch's ~3.6)
 size_t gs_waves_per_launch(const Launch& a) {
-    const size_t cap = kGsWorkspaceCap / gs_bytes_per_wave(a);
+    const size_t floor_w = (size_t)(a.cus > 0 ? a.cus : 256) * 32;
+    size_t cap = kGsWorkspaceCap / gs_bytes_per_wave(a);
+    if (cap < floor_w) cap = floor_w;
     const size_t w = gs_waves(a);
-    return w < cap ? w : (cap > 0 ? cap : 1);
+    if (w <= cap) return w;
+    const size_t launches = (w + cap - 1) / cap;
+    return (w + launches - 1) / launches;
 }
 
 template <int S, bool SOFT>

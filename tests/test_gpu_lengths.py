@@ -129,7 +129,10 @@ def test_large_batch_long_frames(orc, name):
     R = 1 if K <= 7 else (1 << (K - 1)) // 64
     Fw = 64 >> (K - 1) if K <= 6 else 1  # frames per wave
     per_wave = (L + K - 1) * R * 8
-    F = ((1 << 30) // per_wave + 5) * Fw + 3  # just past one launch (K = 3: 131,139 frames, 2.1 GB of input)
+    # waves per launch: 1 GiB of words, at least the 32 per CU the device holds (vtb_lds_path.hip
+    # gs_waves_per_launch); just past that (K = 3: 131,139 frames, 2.1 GB of input)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    F = (max((1 << 30) // per_wave, 32 * cus) + 5) * Fw + 3
     unc, x = random_frames(orc, K, L, 64, 0.04, 5 + K, g=g)
     reps = (F + 63) // 64
     xd = torch.from_numpy(np.ascontiguousarray(x)).cuda().repeat(reps, 1)[:F].contiguous()

@@ -179,6 +179,66 @@ __global__ __launch_bounds__(64) void k1f(uint64_t* out, int iters, uint32_t see
     if ((M ^ acc) == 0x12345678u) out[1 << 20] = M;
 }
 
+// Round 6: the half-partner layout (two frames per wave as lanes 0-31 / 32-63, a lane's two u16
+// halves holding one frame's locations l and l ^ 32): the bit-5 butterfly is inside the register
+// (no v_permlane32_swap), bits 0-3 DPP and bit 4 the permlane16 swap as shipped; everything else
+// (history, table reads from LDS, stores) as k1f.  OPSEL: the partner candidate as one VOP3P
+// v_pk_add_u16 with the source halves swapped (true), or a plain add of a half-swapped table
+// value with the min taking the sum back through op_sel (false).
+__device__ __forceinline__ uint32_t pk_min_sw(uint32_t a, uint32_t b) {
+    const u16x2 bv = __builtin_bit_cast(u16x2, b);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_shufflevector(bv, bv, 1, 0)));
+}
+template <bool OPSEL>
+__global__ __launch_bounds__(64) void k1h(uint64_t* out, int iters, uint32_t seed) {
+    __shared__ uint2 tab[64 * 32];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 64 * 32; i += 64) tab[i] = make_uint2((seed * i) & 0x01ff01ffu, (seed ^ (i * 77)) & 0x01ff01ffu);
+    __syncthreads();
+    uint32_t M = 8192u * 0x10001u + lane, pw = lane, acc = 0;
+    uint2 vb[4][6];
+    for (int g = 0; g < 4; g++)
+        for (int i = 0; i < 6; i++) vb[g][i] = tab[lane + 64 * ((6 * g + i) & 31)];
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; it++) {
+        const int rot = (it & 7) * 4;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            uint2* vw = vb[g];
+            {
+                const uint32_t A = M + vw[0].x;
+                if (OPSEL) {
+                    uint32_t B;
+                    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(B) : "v"(M), "v"(vw[0].y));
+                    M = pk_min(A, B);
+                } else {
+                    M = pk_min_sw(A, M + vw[0].y);
+                }
+            }
+            {
+                uint32_t A = M + vw[1].x, m = M;
+                asm volatile("v_permlane16_swap_b32 %0, %0\n\ts_nop 0" : "+v"(m));
+                M = pk_min(A, m + vw[1].y);
+                hist_ops(M, pw, acc);
+                M &= 0xFFFCFFFCu;
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++) vb[(g + 2) & 3][i] = tab[lane + 64 * ((rot + 6 * g + i) & 31)];
+            dppstep<0x128>(M, vw[2]);
+            dppstep<0x141>(M, vw[3]);
+            M &= 0xFFFCFFFCu;
+            dppstep<0x4E>(M, vw[4]);
+            dppstep<0xB1>(M, vw[5]);
+            M &= 0xFFFCFFFCu;
+        }
+        asm volatile("ds_write_b32 %0, %1 offset:16384\n\tds_write_b32 %0, %2 offset:16640" ::"v"(lane * 4), "v"(acc), "v"(pw));
+        asm volatile("ds_write_b32 %0, %1 offset:20480\n\tds_write_b32 %0, %2 offset:20736" ::"v"(lane * 4), "v"(M), "v"(acc));
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x] = t1 - t0;
+    if ((M ^ acc) == 0x12345678u) out[1 << 20] = M;
+}
+
 __global__ __launch_bounds__(64) void k2f(uint64_t* out, int iters, uint32_t seed) {
     __shared__ uint2 tab[64 * 32];
     const int lane = threadIdx.x;
@@ -240,11 +300,20 @@ double run(F kern, int cus, int wps, int pairs_per_wave, double mhz) {
     return ms * 1e-3 * mhz * 1e6 / (double(steps) * pairs_per_wave * wps);
 }
 
-int main() {
+int main(int argc, char** argv) {
     hipDeviceProp_t p;
     (void)hipGetDeviceProperties(&p, 0);
     const double mhz = 2400.0;
     const int cus = p.multiProcessorCount;
+    if (argc > 1 && argv[1][0] == 'h') {
+        // round 6: shipped vs the half-partner layout, interleaved, five rounds
+        for (int r = 0; r < 5; r++)
+            for (int wps : {2, 4})
+                printf("round %d W=%d: shipped %.2f  half-partner (VOP3P add) %.2f  half-partner (op_sel min) %.2f  "
+                       "cycles per frame-pair-step per SIMD\n",
+                       r, wps, run(k1f, cus, wps, 1, mhz), run(k1h<true>, cus, wps, 1, mhz), run(k1h<false>, cus, wps, 1, mhz));
+        return 0;
+    }
     for (int wps : {1, 2, 4}) {
         printf("W=%d waves/SIMD: shipped C=1 %.2f  shipped C=2 %.2f  two-register %.2f  cycles per frame-pair-step per SIMD\n",
                wps, run(k1<1>, cus, wps, 1, mhz), run(k1<2>, cus, wps, 2, mhz), run(k2, cus, wps, 2, mhz));
