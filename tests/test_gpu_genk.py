@@ -27,7 +27,7 @@ def gpu_present():
 
 
 @pytest.mark.parametrize("code", GENK_CODES, ids=lambda c: f"k{c[0]}K{c[1]}n{len(c[2])}")
-@pytest.mark.parametrize("L,F,p", [(48, 7, 0.1), (1032, 300, 0.04), (2040, 65, 0.0)])
+@pytest.mark.parametrize("L,F,p", [(48, 7, 0.1), (1032, 300, 0.04), (2040, 65, 0.0), (16320, 5, 0.04), (16368, 3, 0.0)])
 def test_genk_gpu_vs_oracle(orc, code, L, F, p):
     k, K, g = code
     unc, coded = genk_frames(orc, k, K, g, L, F, p, L + F + k)
