@@ -54,6 +54,7 @@ struct vtb_plan {
     int seg_warm = 0;
     int seg9_wgs = 0;            // K = 9 SEG kernel workgroups (0: not usable for this plan)
     int seg9_waves = 0;          // and waves per workgroup
+    int segg_waves = 0;          // generic SEG kernel (K = 3..6, 8) waves (0: not usable for this plan)
     // adaptive SEG warm-up (vtb_decode_frame_sync): the short warm-up while frames converge
     // with it; after a miss, the plan's warm-up for `seg_backoff` calls (doubling per miss)
     bool seg_short = false;
@@ -1057,6 +1058,7 @@ static int lat_undo(vtb_plan_t* plan, int err) {
     if (plan->lat_done) (void)hipHostFree(plan->lat_done);
     plan->seg9_ws = nullptr;
     plan->seg9_wgs = plan->seg9_waves = 0;
+    plan->segg_waves = 0;
     plan->lat_in = plan->lat_out = nullptr;
     plan->lat_done = nullptr;
     plan->lat_d_in = plan->lat_d_out = nullptr;
@@ -1124,6 +1126,15 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
             plan->seg9_wgs = wgs;
             plan->seg9_waves = w9;
         }
+        // every other K (3..6, 8): the generic kernel's segments, eight waves ($VTB_SEG_WAVES:
+        // measurement), the short warm-up first as above
+        if (any && !(kn.dbg & 1024) && plan->seg_waves == 0 && plan->seg9_wgs == 0) {
+            const int wg = kn.seg_waves > 0 ? kn.seg_waves : 8;
+            if (vtb::gen_seg_supported(a, wg, warm)) {
+                plan->segg_waves = wg;
+                plan->seg_short = short_ok && vtb::gen_seg_supported(a, wg, vtb::kSegWarmShort);
+            }
+        }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_out), plan->lat_out, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_done), plan->lat_done, 0) != hipSuccess)
@@ -1155,9 +1166,12 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         a.dbg = plan->knobs.dbg;
         a.seg9_xcd = plan->knobs.seg9_xcd;
         a.guard_hits = vtb::debug_guard_hits();
+        a.tstamp = vtb::debug_tstamp();  // (measurement only: gen_seg's phase times)
         std::memcpy(a.symm, plan->symm, sizeof(a.symm));
         if (plan->seg_waves > 0) {
             if (vtb::launch_k7_seg(a, plan->seg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+        } else if (plan->segg_waves > 0) {
+            if (vtb::launch_gen_seg(a, plan->segg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
         } else {
             a.ws = plan->seg9_ws;
             if (vtb::launch_k9_seg(a, plan->seg9_waves, plan->seg9_wgs, warm, d_done) != hipSuccess)
@@ -1180,8 +1194,8 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         g_seg_stats[v == 1 ? 0 : 1]++;
         return VTB_OK;
     };
-    if (plan->seg_waves > 0 || plan->seg9_wgs > 0) {
-        const int wsafe = plan->seg_waves > 0 ? plan->seg_warm : vtb::kSeg9Warm;
+    if (plan->seg_waves > 0 || plan->seg9_wgs > 0 || plan->segg_waves > 0) {
+        const int wsafe = plan->seg_waves > 0 || plan->segg_waves > 0 ? plan->seg_warm : vtb::kSeg9Warm;
         int st = 0;
         if (plan->seg_short && plan->seg_skip == 0) {
             // the short warm-up first: any converged decode is exact, a miss costs one more launch

@@ -77,13 +77,15 @@ void set_debug_tstamp(unsigned long long* p);
 //   known from the frame end skips its checks and re-walks and takes the guard's exact slow
 //   path), 18 K=9 frames on the pair kernel (two frames per wave) where one frame per wave (k9s)
 //   would run, 19 the generic kernel's global-survivor variant (vtb_lds_path.hip GS) for every
-//   frame length.
+//   frame length (its production choice since round 6's register-resident trellis), 20 the
+//   generic kernel's LDS variant wherever its LDS fits one CU.
 // Output-corrupting (phase timing only): 0 skip the traceback, 1 skip the ACS, 2 skip the
 //   traceback verification, 3 warm-up walk only, 4 return at entry.  Only a -DVTB_MEASURE
 //   build (tools/build_variants.sh) honours them; the shipped library masks them off.
 constexpr int kDbgUnsafe = 0x1F;
 constexpr int kDbgTbCap = 1 << 17;
 constexpr int kDbgGenericGs = 1 << 19;
+constexpr int kDbgGenericLds = 1 << 20;
 #ifdef VTB_MEASURE
 constexpr int kDbgHonoured = ~0;
 #else
@@ -141,6 +143,12 @@ bool lds_path_supported(const Launch& a);
 bool lds_path_global(const Launch& a);
 size_t lds_path_workspace_bytes(const Launch& a);
 hipError_t launch_lds_path(const Launch& a);
+// The single-frame path of the generic kernel (gen_seg_kernel, K = 3..6 and 8): one frame
+// (Launch::frames = 1) from host-mapped memory as segments over `waves` waves of one workgroup,
+// warm-up `warm` steps, *done as for K=7's SEG kernel (1 decoded, 2 not converged: nothing
+// written).
+bool gen_seg_supported(const Launch& a, int waves, int warm);
+hipError_t launch_gen_seg(const Launch& a, int waves, int warm, uint32_t* done);
 
 // K=7, survivors in LDS (vtb_k7_lds.hip): the fast path.
 bool k7_lds_supported(const Launch& a);

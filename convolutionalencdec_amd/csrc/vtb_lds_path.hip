@@ -1,50 +1,230 @@
-// Baseline gfx950 decoder: "LDS path".
+// Generic gfx950 decoder for every K = 3..9 ("LDS path" kernel family).
 //
-// One wave64 decodes F = 64/G frames; each frame's N = 2^S trellis states are spread over
-// G = min(N, 64) lanes with R = N/G states per lane in registers (state s lives in lane
-// s % G, register s / G).  Per trellis step every lane gathers the two predecessor
-// metrics of each of its states with ds_bpermute (predecessors of s are s>>1 and
-// (s>>1) + N/2, reference viterbiDecoderButterflyk1.c:101-152), does the add-compare-
-// select, and the wave's __ballot of the decisions (one 64-bit word per register per
-// step) is written to LDS.  After the last step the traceback (reference :200-256) walks
-// the LDS survivor words from state 0.
+// One wave64 decodes F = 64/G frames; each frame's N = 2^S trellis states sit in G = min(N, 64)
+// lanes, R = N/G per lane in registers.  The states move with the step (vtb_k7_lds.hip's in-place
+// butterfly, generalised to every S): at step t, phase ph = t mod S, location l holds state
+// rotl_S(l, ph).  The two predecessors of a butterfly, j and j + N/2 (reference
+// viterbiDecoderButterflyk1.c:101-152), are then a location and its partner across location bit
+// p = S-1-ph, and the butterfly's destinations 2j and 2j+1 land back in those two locations
+// (location l receives state rotl_S(l, ph+1)).  So the gather is one DPP (p = 0..3: lane XOR 1, 2,
+// 7, 8 under the lane <-> location involution lane_of), a v_permlane16/32_swap (p = 4, 5) or the
+// lane's other register (p >= 6): the recursion never leaves the VGPRs.  Per step and register:
+// the branch metric (one v_dot2), the two candidates, two compares whose wave masks combine (with
+// the constant mask of the lanes holding the upper predecessor) into the decision word, and a min.
+// Decision bit of the state a location receives = bit (lane) of the wave's word: 1 = the upper
+// predecessor won (strict compare, ties keep the lower: reference :129-130).
 //
-// This is the simple, obviously-correct kernel: the register-resident kernel
-// (vtb_k7_lds.hip) is the fast path; this one also covers every K in 3..9.
-//
-// Two variants of the one kernel (template parameter GS; lds_path_global picks one):
-//   * LDS: every survivor word and the wave's whole input in LDS, 8 R T + F T B bytes per wave
-//     (B = 1 hard, 2 soft) -- K = 3, 4 frames of 2,048+ steps while that LDS leaves the CU
-//     the batch's waves;
-//   * GS (global survivors): the survivor words in a global workspace (8 R T bytes per wave,
-//     the lane that owns step t mod 64 keeps its ballot words in registers and the wave stores
-//     64 steps' words at once, coalesced), the input staged through LDS kStage steps at a time
-//     (F kStage B bytes), the traceback reading the words back from L2/HBM.  Every frame up to
-//     VTB_MAX_FRAME_BITS (the reference's MAX_PKT_LEN_UNCODED_BITS, viterbiDecoder.h:18), at
-//     any K, hard or soft (VERDICT r5 missing #1).
+// Survivor words: the lane that owns step t mod C (C = P floor(64/P), P = the loop body's steps,
+// a multiple of S: whole phase cycles) keeps
+// the step's R words in registers (v_writelane) and the wave stores C steps' words at once,
+// coalesced.  Two variants (template parameter GS; lds_path_global picks one):
+//   * LDS: the survivor words and the wave's whole input in LDS, 8 R T + F T B bytes per wave
+//     (B = 1 hard, 2 soft) -- K = 3, 4 frames of 2,048+ steps while that LDS leaves the CU the
+//     batch's waves;
+//   * GS (global survivors): the survivor words in a global workspace (8 R T bytes per wave), the
+//     input staged through LDS C steps at a time, the traceback reading the words back from L2 /
+//     HBM.  Every frame up to VTB_MAX_FRAME_BITS (the reference's MAX_PKT_LEN_UNCODED_BITS,
+//     viterbiDecoder.h:18), at any K, hard or soft.
 // Decisions, metrics and traceback are the same code in both: the outputs are identical.
 //
+// Traceback in locations: with k = (t+1) mod S the state after step t is d = rotl_S(loc, k), so
+// its information bit (bit 0 of d) is location bit b = (S - k) mod S, and the predecessor's
+// location after step t-1 is loc with bit b replaced by the decision bit (the walk never rotates).
+//
 #include "vtb_internal.h"
+
+#include <utility>
+
+// v_writelane_b32 (no clang builtin in this toolchain: the LLVM intrinsic by name)
+__device__ int vtb_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 namespace vtb {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
 
-__device__ __forceinline__ int shfl_idx(int v, int src_lane) {
-    return __builtin_amdgcn_ds_bpermute(src_lane << 2, v);
-}
-
-// Decisions for state s at step t:  bit (fi*G + s%G) of word [t][s/G].
 template <int S>
 struct Geometry {
     static constexpr int N = 1 << S;
     static constexpr int G = N < 64 ? N : 64;  // lanes per frame
     static constexpr int R = N / G;            // states per lane
     static constexpr int F = 64 / G;           // frames per wave
+    // the recursion's loop body: U phase cycles, P = U S steps (>= 6: the body outlasts the LDS
+    // latency of the next body's input reads)
+    static constexpr int U = S <= 2 ? 4 : S <= 4 ? 2 : 1;
+    static constexpr int P = U * S;
+    static constexpr int C = P * (64 / P);  // steps per keep/store round: whole loop bodies
 };
 
-constexpr int kStage = 64;  // GS: steps of input staged into LDS per round (= lanes: one keeper per step)
+// host side: steps of one loop body (Geometry<S>::P)
+constexpr int body_steps(int S) { return S <= 2 ? 4 * S : S <= 4 ? 2 * S : S; }
+
+template <int... Is, class Fn>
+__device__ __forceinline__ void gen_static_for(std::integer_sequence<int, Is...>, Fn&& fn) {
+    (fn(std::integral_constant<int, Is>{}), ...);
+}
+
+// lane <-> location involution (location bit 2 set: bits 0, 1 flipped), so that location
+// XOR 4 is lane XOR 7 (DPP row_half_mirror); XOR 1, 2, 8, 16, 32 are unchanged
+template <int S>
+__host__ __device__ constexpr unsigned lane_of(unsigned l) {
+    return S >= 3 ? l ^ (((l >> 2) & 1u) * 3u) : l;
+}
+
+template <int S>
+__device__ __forceinline__ unsigned rotl_s(unsigned x, int k) {
+    return ((x << k) | (x >> (S - k))) & ((1u << S) - 1u);
+}
+
+// Wave masks of the lanes whose register r holds the upper predecessor (location bit p = S-1-ph
+// set) at phase ph: the lanes whose compare is the other way round.
+template <int S>
+struct UpperMasks {
+    uint64_t m[Geometry<S>::R][S];
+};
+template <int S>
+constexpr UpperMasks<S> upper_masks() {
+    UpperMasks<S> u{};
+    for (int r = 0; r < Geometry<S>::R; r++)
+        for (int ph = 0; ph < S; ph++) {
+            uint64_t w = 0;
+            for (int lane = 0; lane < 64; lane++) {
+                const unsigned l = unsigned(r) * 64u + lane_of<S>(unsigned(lane % Geometry<S>::G));
+                if ((l >> (S - 1 - ph)) & 1u) w |= uint64_t(1) << lane;
+            }
+            u.m[r][ph] = w;
+        }
+    return u;
+}
+
+// The partner's metric across location bit P < 6.  For the permlane swaps (in place on a copy)
+// one wait state each way (tools/probes/permlane_hazard.hip).
+template <int P>
+__device__ __forceinline__ int partner(int m) {
+    if constexpr (P == 0) {
+        return __builtin_amdgcn_update_dpp(0, m, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]: XOR 1
+    } else if constexpr (P == 1) {
+        return __builtin_amdgcn_update_dpp(0, m, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]: XOR 2
+    } else if constexpr (P == 2) {
+        return __builtin_amdgcn_update_dpp(0, m, 0x141, 0xF, 0xF, true);  // row_half_mirror: XOR 7
+    } else if constexpr (P == 3) {
+        return __builtin_amdgcn_update_dpp(0, m, 0x128, 0xF, 0xF, true);  // row_ror:8: XOR 8
+    } else if constexpr (P == 4) {
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0\n\ts_nop 0" : "+v"(m));
+        return m;
+    } else {
+        asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0\n\ts_nop 0" : "+v"(m));
+        return m;
+    }
+}
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+// Received pair of one step: the raw bytes (hard: one symbol byte, soft: two bytes), then as
+// the packed operand of v_dot2 (hard: the two bits, soft: the bytes).  The recursion converts a
+// cycle's raw bytes only after the previous cycle's steps, so that their LDS reads are waited for
+// there and not where they are issued.
+template <bool SOFT>
+__device__ __forceinline__ int rx_raw(const uint8_t* p) {
+    if constexpr (SOFT) {
+        return int(p[0]) | (int(p[1]) << 16);
+    } else {
+        return int(p[0]);
+    }
+}
+template <bool SOFT>
+__device__ __forceinline__ int rx_pair(int raw) {
+    if constexpr (SOFT) {
+        return raw;
+    } else {
+        return (raw & 1) | (((raw >> 1) & 1) << 16);
+    }
+}
+
+// Branch-metric coefficients of location l at phase ph: the centred metric of the lower
+// predecessor's edge into the state l receives is v_dot2(sig, rx) + kap, as signed for the
+// location's own candidate (own + mu, partner - mu: the sign of the destination parity cancels
+// against which of the pair the location holds).
+template <int S, int Q>
+__device__ __forceinline__ void coefficients(const Launch& table, unsigned l, int ph, int& sig, int& kap) {
+    const unsigned s = rotl_s<S>(l, ph);
+    const int c = table.symm[s & ((1u << (S - 1)) - 1u)];
+    const int s0 = (c & 1) ? -1 : 1, s1 = (c & 2) ? -1 : 1;
+    sig = (s0 & 0xffff) | (s1 << 16);
+    kap = (((c & 1) + ((c >> 1) & 1)) - 1) * Q;
+}
+
+// One trellis step at phase PH (compile time): metrics m[R] in place, the R decision words out.
+template <int S, int PH, int R>
+__device__ __forceinline__ void rot_step(int (&m)[R], int qp, const int (&sig)[R][S], const int (&kap)[R][S],
+                                         uint64_t (&bal)[R]) {
+    constexpr int P = S - 1 - PH;
+    constexpr UpperMasks<S> UM = upper_masks<S>();
+    int nm[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, sig[r][PH]), __builtin_bit_cast(short2_t, qp),
+                                              kap[r][PH], false);
+        int pm;
+        if constexpr (P >= 6) {
+            pm = m[r ^ (1 << (P - 6))];
+        } else {
+            pm = partner<P>(m[r]);
+        }
+        const int a = m[r] + mu, b = pm - mu;  // own candidate, partner's candidate
+        const uint64_t gt = __ballot(a > b), lt = __ballot(b > a);
+        bal[r] = (gt & ~UM.m[r][PH]) | (lt & UM.m[r][PH]);  // lower's candidate > upper's
+        nm[r] = a < b ? a : b;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) m[r] = nm[r];
+}
+
+// One phase cycle (S steps) from the prepared received pairs q, the decision words kept by lanes
+// i .. i + S - 1 of klo / khi (v_writelane).
+template <int S, int R>
+__device__ __forceinline__ void acs_cycle(int (&m)[R], const int* q, const int (&sig)[R][S], const int (&kap)[R][S],
+                                          uint32_t (&klo)[R], uint32_t (&khi)[R], int i) {
+    gen_static_for(std::make_integer_sequence<int, S>{}, [&](auto pc) {
+        constexpr int PH = decltype(pc)::value;
+        uint64_t bal[R];
+        rot_step<S, PH, R>(m, q[PH], sig, kap, bal);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            klo[r] = uint32_t(vtb_writelane(int(uint32_t(bal[r])), i + PH, int(klo[r])));
+            khi[r] = uint32_t(vtb_writelane(int(uint32_t(bal[r] >> 32)), i + PH, int(khi[r])));
+        }
+    });
+}
+
+// Traceback helpers (locations).  Bit of step t's information bit: b = (S - (t+1) mod S) mod S;
+// b of step t - 1 is b + 1 mod S.
+template <int S>
+__device__ __forceinline__ int info_bit_pos(int t) {
+    const int k = (t + 1) % S;
+    return k == 0 ? 0 : S - k;
+}
+template <int S>
+__device__ __forceinline__ int next_pos(int b) {
+    return b + 1 == S ? 0 : b + 1;
+}
+// The location after step t - 1 from the location after step t, step t's R words and b;
+// `base` = the frame's first lane in the words.
+template <int S, int R>
+__device__ __forceinline__ unsigned tb_step(unsigned loc, const uint64_t (&w)[R], int b, unsigned base) {
+    constexpr unsigned G = unsigned(Geometry<S>::G);
+    const unsigned sh = base + lane_of<S>(loc & (G - 1u));
+    unsigned x[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) x[r] = unsigned(w[r] >> sh) & 1u;  // (bits first: no word select)
+    unsigned d = x[0];
+    if constexpr (R == 2) d = (loc & 64u) ? x[1] : x[0];
+    if constexpr (R == 4) {
+        const unsigned lo2 = (loc & 64u) ? x[1] : x[0], hi2 = (loc & 64u) ? x[3] : x[2];
+        d = (loc & 128u) ? hi2 : lo2;
+    }
+    return (loc & ~(1u << b)) | (d << b);
+}
 
 template <int S, bool SOFT, bool GS>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uint8_t* __restrict__ in, size_t in_stride,
@@ -52,10 +232,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
                                                                         int T, int L, size_t frames, int waves_per_block,
                                                                         Launch table) {
     using Gm = Geometry<S>;
-    constexpr int N = Gm::N, G = Gm::G, R = Gm::R, F = Gm::F;
+    constexpr int N = Gm::N, G = Gm::G, R = Gm::R, F = Gm::F, C = Gm::C;
     constexpr int Q = SOFT ? 255 : 1;
     constexpr int INIT = int(uint8_t(N + 1)) * Q;  // (uint8_t)(NUM_STATES+1), reference :62
-    constexpr int BYTES_PER_SEG = SOFT ? 2 : 1;
+    constexpr int B = SOFT ? 2 : 1;
 
     extern __shared__ uint64_t smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -63,15 +243,20 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     const int fi = lane / G;
     const int lam = lane % G;
 
-    const size_t dec_words = (size_t)T * R;
+    constexpr int P = Gm::P, U = Gm::U;
+    const int TS = (T + P - 1) / P * P;  // steps run: whole loop bodies (decisions past T unused)
+    const size_t dec_words = (size_t)TS * R;
     uint64_t* dec;
     uint8_t* inbuf;
+    int in_row;  // staged bytes per frame
     if constexpr (GS) {
         // one wave per block: the block's slot of the launch's workspace, the staging buffer in LDS
         dec = static_cast<uint64_t*>(table.ws) + (size_t)blockIdx.x * dec_words;
         inbuf = reinterpret_cast<uint8_t*>(smem);
+        in_row = C * B;
     } else {
-        const size_t in_bytes = ((size_t)F * T * BYTES_PER_SEG + 7) & ~size_t(7);
+        in_row = TS * B;
+        const size_t in_bytes = ((size_t)F * in_row + 7) & ~size_t(7);
         dec = smem + (size_t)wave * (dec_words + in_bytes / 8);
         inbuf = reinterpret_cast<uint8_t*>(dec + dec_words);
     }
@@ -80,158 +265,131 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     const size_t myframe = frame0 + fi;
     const bool valid = myframe < frames;
 
-    // Per-register branch-metric coefficients.  Destination d = r*G + lam has
-    // predecessors j = d>>1 and j + N/2; with b = d&1 the candidate from j is m[j] + mu_b
-    // and from j + N/2 is m[j+N/2] - mu_b, where mu_0 = mu(c) and mu_1 = -mu(c).
-    int sig[R], kap[R];
+    const unsigned l0 = lane_of<S>(unsigned(lam));  // this lane's location (register 0)
+    int sig[R][S], kap[R][S], m[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        int d = r * G + lam;
-        int c = table.symm[d >> 1];
-        int sb = (d & 1) ? -1 : 1;
-        int s0 = ((c & 1) ? -1 : 1) * sb, s1 = ((c & 2) ? -1 : 1) * sb;
-        sig[r] = (s0 & 0xffff) | (s1 << 16);
-        kap[r] = (((c & 1) + ((c >> 1) & 1)) - 1) * Q * sb;
+        const unsigned l = unsigned(r) * 64u + l0;
+#pragma unroll
+        for (int ph = 0; ph < S; ph++) coefficients<S, Q>(table, l, ph, sig[r][ph], kap[r][ph]);
+        m[r] = l == 0 ? 0 : INIT;  // phase 0: location = state
     }
 
-    int m[R];
+    uint32_t klo[R], khi[R];  // lane i keeps the words of step c0 + i
 #pragma unroll
-    for (int r = 0; r < R; r++) m[r] = (r * G + lam == 0) ? 0 : INIT;
-
-    const int src_base = fi * G;
-    // One trellis step from the frame's received pair at `seg`: the R ballot words out.
-    auto acs_step = [&](const uint8_t* seg, uint64_t* ballots) {
-        int qp;
-        if (SOFT) {
-            qp = int(seg[0]) | (int(seg[1]) << 16);
-        } else {
-            int c = seg[0];
-            qp = (c & 1) | (((c >> 1) & 1) << 16);
-        }
-        int nm[R];
+    for (int r = 0; r < R; r++) klo[r] = khi[r] = 0;
+    // the received pairs of the P steps at p (read one loop body ahead of their use: the LDS
+    // latency off the recursion's chain)
+    auto load_q = [&](const uint8_t* p, int (&q)[P]) {
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int lane0 = src_base + (r & 1) * (G / 2) + (lam >> 1);
-            int a0, a1;
-            if (R == 1) {
-                a0 = shfl_idx(m[0], lane0);
-                a1 = shfl_idx(m[0], lane0 + G / 2);
-            } else {
-                a0 = shfl_idx(m[r >> 1], lane0);
-                a1 = shfl_idx(m[(r >> 1) + R / 2], lane0);
-            }
-            typedef short short2_t __attribute__((ext_vector_type(2)));
-            int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, sig[r]), __builtin_bit_cast(short2_t, qp),
-                                            kap[r], false);
-            int c0 = a0 + mu, c1 = a1 - mu;
-            bool d = c0 > c1;  // strict: ties keep the lower predecessor (reference :129-130)
-            nm[r] = d ? c1 : c0;
-            ballots[r] = __ballot(d);
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) m[r] = nm[r];
+        for (int j = 0; j < P; j++) q[j] = rx_raw<SOFT>(p + j * B);
     };
 
-    if constexpr (GS) {
-        constexpr int kRow = kStage * BYTES_PER_SEG;  // staged bytes per frame
-        const uint8_t* myin = inbuf + fi * kRow;
-        for (int c0 = 0; c0 < T; c0 += kStage) {
-            const int n = T - c0 < kStage ? T - c0 : kStage;
-            const int nb = n * BYTES_PER_SEG;
-            __syncthreads();  // (one wave: the previous round's reads of the buffer are done)
-            for (int idx = lane; idx < F * nb; idx += 64) {
-                const int f = idx / nb, off = idx - f * nb;
-                inbuf[f * kRow + off] =
-                    frame0 + f < frames ? in[(frame0 + f) * in_stride + (size_t)c0 * BYTES_PER_SEG + off] : 0;
-            }
-            __syncthreads();
-            uint64_t keep[R];  // lane i keeps the words of step c0 + i
-#pragma unroll
-            for (int r = 0; r < R; r++) keep[r] = 0;
-            for (int i = 0; i < n; i++) {
-                uint64_t ballots[R];
-                acs_step(myin + i * BYTES_PER_SEG, ballots);
-#pragma unroll
-                for (int r = 0; r < R; r++) keep[r] = lane == i ? ballots[r] : keep[r];
-            }
-            if (lane < n) {
-#pragma unroll
-                for (int r = 0; r < R; r++) dec[(size_t)(c0 + lane) * R + r] = keep[r];
-            }
-        }
-        __threadfence_block();  // the survivor words before any lane's traceback reads them
-    } else {
-        // Stage this wave's input frames into LDS (coalesced byte loads).
-        const int seg_bytes = T * BYTES_PER_SEG;
-        for (int idx = lane; idx < F * seg_bytes; idx += 64) {
-            int f = idx / seg_bytes, off = idx - f * seg_bytes;
+    const uint8_t* myin = inbuf + fi * in_row;
+    if constexpr (!GS) {
+        // the wave's input frames into LDS (coalesced byte loads; zero past T)
+        for (int idx = lane; idx < F * in_row; idx += 64) {
+            const int f = idx / in_row, off = idx - f * in_row;
             uint8_t v = 0;
-            if (frame0 + f < frames) v = in[(frame0 + f) * in_stride + off];
+            if (frame0 + f < frames && off < T * B) v = in[(frame0 + f) * in_stride + off];
             inbuf[idx] = v;
         }
         __syncthreads();
-        const uint8_t* myin = inbuf + fi * seg_bytes;
-        for (int t = 0; t < T; t++) {
-            uint64_t ballots[R];
-            acs_step(myin + t * BYTES_PER_SEG, ballots);
-            if (lane == 0) {
+    }
+    // GS: the input of the next C steps is loaded into registers (kPf bytes per lane) while this
+    // chunk's steps run, and written to the other half of the staging buffer after them
+    constexpr int kPf = (F * C * B + 63) / 64;
+    uint32_t pf[GS ? kPf : 1];
+    auto fetch = [&](int c0) {
 #pragma unroll
-                for (int r = 0; r < R; r++) dec[(size_t)t * R + r] = ballots[r];
+        for (int j = 0; j < kPf; j++) {
+            const int idx = lane + 64 * j, f = idx / (C * B), off = idx - f * (C * B), src = c0 * B + off;
+            pf[j] = f < F && frame0 + f < frames && src < T * B ? in[(frame0 + f) * in_stride + (size_t)src] : 0u;
+        }
+    };
+    auto commit = [&](uint8_t* buf) {
+#pragma unroll
+        for (int j = 0; j < kPf; j++)
+            if (lane + 64 * j < F * C * B) buf[lane + 64 * j] = uint8_t(pf[j]);
+    };
+    if constexpr (GS) {
+        fetch(0);
+        commit(inbuf);
+        __syncthreads();
+    }
+    for (int c0 = 0, k = 0; c0 < TS; c0 += C, k ^= 1) {
+        const int n = TS - c0 < C ? TS - c0 : C;  // a multiple of S
+        const uint8_t* base;
+        if constexpr (GS) {
+            if (c0 + C < TS) fetch(c0 + C);
+            base = myin + k * (F * C * B);
+        } else {
+            base = myin + c0 * B;
+        }
+        int q[P];
+        load_q(base, q);
+#pragma unroll
+        for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(q[j]);
+        for (int i = 0; i < n; i += P) {  // (n: a multiple of P)
+            int qn[P];
+            load_q(base + (i + P < n ? i + P : i) * B, qn);
+#pragma unroll
+            for (int u = 0; u < U; u++) acs_cycle<S, R>(m, q + u * S, sig, kap, klo, khi, i + u * S);
+#pragma unroll
+            for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(qn[j]);
+        }
+        if (lane < n) {
+#pragma unroll
+            for (int r = 0; r < R; r++) dec[(size_t)(c0 + lane) * R + r] = uint64_t(klo[r]) | (uint64_t(khi[r]) << 32);
+        }
+        if constexpr (GS) {
+            if (c0 + C < TS) {
+                commit(inbuf + (k ^ 1) * (F * C * B));
+                __syncthreads();
             }
         }
     }
+    if constexpr (GS) __threadfence_block();  // the survivor words before any lane's traceback reads them
 
     __syncthreads();
     if (!valid) return;
 
     // Terminated traceback from state 0 (reference :200-256), block-parallel and verified
-    // (the K=7 kernel's scheme, vtb_k7_lds.hip): the frame's G lanes each take a block of tbb
-    // steps (a multiple of 8: every block owns whole output bytes), walk back to it from
-    // kWarm steps past its end starting in state 0 there (exact when that is T, the
-    // terminated end), and a block is right once it entered on its successor's exit state and
-    // that successor is proven; failed blocks re-walk from a proven successor until all are.
-    // The state after step t is s; its bit 0 is the information bit of step t, and the
-    // predecessor is (s >> 1) | (decision << (S - 1)).
+    // (DESIGN.md §4.0): the frame's G lanes each take a block of tbb steps (a multiple of 8:
+    // every block owns whole output bytes), walk back to it from kWarm steps past its end starting
+    // in state 0 there (exact when that is T, the terminated end), and a block is right once it
+    // entered on its successor's exit location and that successor is proven; failed blocks re-walk
+    // from a proven successor until all are.  Walks carry locations (state 0 is location 0).
     constexpr int kWarm = 8 * S + 48;
-    // A step's R survivor words do not depend on the walk's state (only the bit taken from them
+    // A step's R survivor words do not depend on the walk's location (only the bit taken from them
     // does), so the walks load kTb steps' words at once and then take the kTb dependent steps:
     // kTb loads in flight instead of one (GS: L2 / HBM latency; LDS: ds_read latency).
-    constexpr int kTb = R == 4 ? 4 : 8;
+    constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
+    const unsigned fbase = unsigned(fi * G);
     auto row = [&](int t, uint64_t (&w)[R]) {
 #pragma unroll
         for (int r = 0; r < R; r++) w[r] = dec[(size_t)t * R + r];
     };
-    // (each word's bit is taken before the select: a select between the 64-bit words is
-    // compiled as a dynamically indexed array in scratch memory)
-    auto step = [&](unsigned st, const uint64_t (&w)[R]) -> unsigned {
-        const unsigned sh = unsigned(fi * G) + (st % G);
-        unsigned b[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) b[r] = unsigned(w[r] >> sh) & 1u;
-        unsigned x = b[0];
-        if constexpr (R == 2) x = (st & unsigned(G)) ? b[1] : b[0];
-        if constexpr (R == 4) {
-            const unsigned lo2 = (st & unsigned(G)) ? b[1] : b[0], hi2 = (st & unsigned(G)) ? b[3] : b[2];
-            x = (st & unsigned(2 * G)) ? hi2 : lo2;
-        }
-        return (st >> 1) | (x << (S - 1));
-    };
-    // the state before steps [lo, hi) given the state after step hi - 1
-    auto walk = [&](unsigned st, int hi, int lo) -> unsigned {
-        int t = hi;
+    // the location before steps [lo, hi) given the location after step hi - 1
+    auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {
+        int t = hi, b = info_bit_pos<S>(hi - 1);
         for (; t - kTb >= lo; t -= kTb) {
             uint64_t w[kTb][R];
 #pragma unroll
             for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
 #pragma unroll
-            for (int j = 0; j < kTb; j++) st = step(st, w[j]);
+            for (int j = 0; j < kTb; j++) {
+                loc = tb_step<S, R>(loc, w[j], b, fbase);
+                b = next_pos<S>(b);
+            }
         }
         for (; t > lo; t--) {
             uint64_t w[R];
             row(t - 1, w);
-            st = step(st, w);
+            loc = tb_step<S, R>(loc, w, b, fbase);
+            b = next_pos<S>(b);
         }
-        return st;
+        return loc;
     };
     const int tbb = ((T + G - 1) / G + 7) / 8 * 8;
     const int lo = lam * tbb, top = lo + tbb < T ? lo + tbb : T;
@@ -250,7 +408,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     const int rounds = tbforce ? 0 : G + 1;
     uint64_t unproven = 0;
     for (int round = 0;; round++) {
-        const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
+        const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry location
         const bool ok = fixed || (s_top == sf && !tbforce);
         const uint64_t bad = ~__ballot(ok);
         if (bad == 0) break;
@@ -272,23 +430,24 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         if (lam == 0 && valid) note_guard(table.guard_hits);
     }
     if (!valid || !emit) return;
-    // Emission, MSB-first bytes (reference :243-249): bit t of the frame is bit 0 of the state
-    // after step t; byte t / 8 is complete at step t = 0 mod 8 (elo is a multiple of 8).  The
-    // steps above the last whole octet of [elo, etop) one by one, then octets with their 8 rows
-    // loaded at once.
+    // Emission, MSB-first bytes (reference :243-249): bit t of the frame is the information bit
+    // of the location after step t; byte t / 8 is complete at step t = 0 mod 8 (elo is a
+    // multiple of 8).  The steps above the last whole octet of [elo, etop) one by one, then
+    // octets with their 8 rows loaded at once.
     uint8_t* o = out + myframe * out_stride;
     unsigned byte = 0;
     st = s_top;
     auto put = [&](int t) {
         if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
     };
-    int t = etop - 1;
+    int t = etop - 1, b = info_bit_pos<S>(etop - 1);
     for (; t >= elo && ((t + 1) & 7) != 0; t--) {
-        byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
+        byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
         if ((t & 7) == 0) put(t);
         uint64_t w[R];
         row(t, w);
-        st = step(st, w);
+        st = tb_step<S, R>(st, w, b, fbase);
+        b = next_pos<S>(b);
     }
     for (; t >= elo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
         uint64_t w[8][R];
@@ -296,8 +455,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         for (int j = 0; j < 8; j++) row(t - j, w[j]);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            byte = ((byte >> 1) | ((st & 1u) << 7)) & 0xffu;
-            st = step(st, w[j]);
+            byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
+            st = tb_step<S, R>(st, w[j], b, fbase);
+            b = next_pos<S>(b);
         }
         put(t - 7);
     }
@@ -306,8 +466,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
 template <int S>
 size_t lds_bytes_per_wave(int soft, int T) {
     using Gm = Geometry<S>;
-    size_t dec = (size_t)T * Gm::R * 8;
-    size_t inb = ((size_t)Gm::F * T * (soft ? 2 : 1) + 7) & ~size_t(7);
+    const size_t TS = size_t(T + Geometry<S>::P - 1) / Geometry<S>::P * Geometry<S>::P;  // whole loop bodies
+    size_t dec = TS * Gm::R * 8;
+    size_t inb = ((size_t)Gm::F * TS * (soft ? 2 : 1) + 7) & ~size_t(7);
     return dec + inb;
 }
 
@@ -331,7 +492,10 @@ constexpr size_t kGsWorkspaceCap = size_t(1) << 30;
 
 int states_per_lane(int S) { return S <= 6 ? 1 : (1 << S) / 64; }
 int frames_per_wave(int S) { return S >= 6 ? 1 : 64 >> S; }
-size_t gs_bytes_per_wave(const Launch& a) { return (size_t)a.T * states_per_lane(a.S) * 8; }
+size_t gs_bytes_per_wave(const Launch& a) {
+    const size_t P = size_t(body_steps(a.S));
+    return (size_t(a.T) + P - 1) / P * P * states_per_lane(a.S) * 8;
+}
 size_t gs_waves(const Launch& a) { return (a.frames + frames_per_wave(a.S) - 1) / frames_per_wave(a.S); }
 // Waves per launch: at most 1 GiB of survivor words, but never fewer than the CUs hold at once
 // (32 per CU), and the launches of one batch balanced -- a remainder launch of a few waves runs a
@@ -353,7 +517,7 @@ hipError_t launch_typed(const Launch& a) {
     if (lds_path_global(a)) {
         // one wave per block; launches of at most gs_waves_per_launch waves over the workspace
         const size_t per = gs_waves_per_launch(a), waves = gs_waves(a);
-        const size_t lds = (size_t)Gm::F * kStage * (SOFT ? 2 : 1);
+        const size_t lds = 2 * (size_t)Gm::F * Gm::C * (SOFT ? 2 : 1);  // two staging halves
         for (size_t w0 = 0; w0 < waves; w0 += per) {
             const size_t nw = waves - w0 < per ? waves - w0 : per;
             const size_t f0 = w0 * Gm::F;
@@ -398,7 +562,363 @@ hipError_t launch_soft(const Launch& a) {
     }
 }
 
+
+// ---------------- single-frame latency path for every K (gen_seg_kernel) ----------------
+//
+// vtb_decode_frame_sync for the codes without a SEG kernel of their own (K = 3..6, 8; K = 7 and
+// K = 9 have k7_seg / k9_seg): one frame at a time is one dependent chain of T steps, so the frame
+// is cut into G segments decoded at once by the F = 64 / min(N, 64) frame slots of each of up to
+// eight waves of one workgroup (the batch kernel's trellis layout and arithmetic above).  Segment
+// i runs n steps from g_i = i (n - warm); segment 0 starts from the reference's start metrics,
+// the others from equal metrics.  Segment i's decisions are the frame's from s_i = g_i + warm on
+// when its metric vector there equals segment i - 1's final one up to a constant (the trellis
+// compares differences only; segment i - 1 is exact up to s_i by induction) -- vtb_k7_lds.hip's
+// SEG argument.  n and warm are whole loop bodies (P steps, a multiple of S: every g_i is one, all slots of a
+// wave share the phase, and the boundary compares happen at phase 0, where location = state).
+// If every boundary holds, wave 0 traces the frame back over all segments' words (64 blocks,
+// verified chains, completeness guard) and writes the bytes; else nothing is
+// written and *done = 2 (the host decodes the frame with the batch kernel).  Input from and
+// output to host-mapped memory, *done = 1 with a system-scope release at the end.
+struct GenSeg {
+    int n = 0, warm = 0, G = 0, W = 0;  // steps per segment, warm-up, segments, waves
+    int in_lds = 0;                     // LDS byte offset of the staged input, later the decoded bytes
+                                        // (the frame's survivor rows, T R 8 bytes, from offset 0)
+    int x_lds = 0;                      // exchange: final metrics [G][N], warm-up metrics [G][N], ok [G]
+    uint32_t* done = nullptr;           // completion word (host-mapped) or null
+};
+
+constexpr int kGenSegStage = 4;  // 16-byte staging loads per thread issued before their stores (v0..v3)
+
+template <int S, bool SOFT>
+__global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int T,
+                                                      int L, Launch table, GenSeg sg) {
+    using Gm = Geometry<S>;
+    constexpr int N = Gm::N, G = Gm::G, R = Gm::R, F = Gm::F, C = Gm::C;
+    constexpr int Q = SOFT ? 255 : 1;
+    constexpr int INIT = int(uint8_t(N + 1)) * Q;  // reference :62
+    constexpr int B = SOFT ? 2 : 1;
+    extern __shared__ uint64_t smem[];
+    uint8_t* sm = reinterpret_cast<uint8_t*>(smem);
+    const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
+    const int fi = lane / G, lam = lane % G;
+    // Measurement only (Launch::tstamp, tools/tstamp_seg.py): wave 0's phase times, 100 MHz
+    // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 4 chains proven,
+    // 5 bytes assembled, 6 output written; 7 = core clocks from 0 to 6
+    const uint64_t clk0 = table.tstamp ? __builtin_amdgcn_s_memtime() : 0;
+    auto ts = [&](int k) {
+        if (table.tstamp && threadIdx.x == 0) table.tstamp[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    ts(0);
+
+    // the frame's input into LDS: rounds of up to four 16-byte loads per thread, all issued before
+    // their stores (the host-mapped buffer is padded to 16 bytes)
+    {
+        const int nin = B * T, step = 16 * int(blockDim.x);
+        // (loads past the frame read the buffer's last chunk again: clamped, never stored; named
+        // registers, not an array, which the compiler placed in scratch)
+        const int last = (nin - 1) & ~15;
+        auto ld = [&](int o) { return *reinterpret_cast<const uint4*>(in + (o < nin ? o : last)); };
+        auto stl = [&](int o, uint4 v) {
+            if (o < nin) *reinterpret_cast<uint4*>(sm + sg.in_lds + o) = v;
+        };
+        for (int base = 16 * int(threadIdx.x); base < nin; base += kGenSegStage * step) {
+            const uint4 v0 = ld(base), v1 = ld(base + step), v2 = ld(base + 2 * step), v3 = ld(base + 3 * step);
+            stl(base, v0), stl(base + step, v1), stl(base + 2 * step, v2), stl(base + 3 * step, v3);
+        }
+    }
+    __syncthreads();
+    ts(1);
+
+    const int seg = wv * F + fi;  // this slot's segment
+    const int sstep = sg.n - sg.warm;
+    const int g0 = seg * sstep;  // a multiple of S
+    const unsigned l0 = lane_of<S>(unsigned(lam));
+    int sig[R][S], kap[R][S], m[R], mw[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const unsigned l = unsigned(r) * 64u + l0;
+#pragma unroll
+        for (int ph = 0; ph < S; ph++) coefficients<S, Q>(table, l, ph, sig[r][ph], kap[r][ph]);
+        m[r] = seg == 0 ? (l == 0 ? 0 : INIT) : 0;
+        mw[r] = m[r];
+    }
+    // survivor rows of the frame: step t's R words (this frame's G bits from bit 0) at row t,
+    // written by the one segment whose decisions are the frame's there (segment 0: local steps
+    // [0, n), segment i: [warm, n), i.e. [s_i, s_(i+1)))
+    uint64_t* rows = reinterpret_cast<uint64_t*>(sm);
+    const uint8_t* inb = sm + sg.in_lds;
+    uint32_t klo[R], khi[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) klo[r] = khi[r] = 0;
+    // the received pairs of local steps t .. t + P - 1, read one loop body ahead of their use
+    // (steps past the frame: any input, their decisions unused)
+    constexpr int P = Gm::P, U = Gm::U;
+    auto load_q = [&](int t, int (&q)[P]) {
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            const int tg = g0 + t + j;
+            q[j] = rx_raw<SOFT>(inb + (tg < T ? tg : T - 1) * B);
+        }
+    };
+    int q[P];
+    load_q(0, q);
+#pragma unroll
+    for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(q[j]);
+    for (int c0 = 0; c0 < sg.n; c0 += C) {
+        const int nn = sg.n - c0 < C ? sg.n - c0 : C;  // a multiple of P
+        for (int i = 0; i < nn; i += P) {
+            int qn[P];
+            load_q(c0 + i + P, qn);
+#pragma unroll
+            for (int u = 0; u < U; u++) acs_cycle<S, R>(m, q + u * S, sig, kap, klo, khi, i + u * S);
+#pragma unroll
+            for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(qn[j]);
+            if (c0 + i + P == sg.warm) {
+#pragma unroll
+                for (int r = 0; r < R; r++) mw[r] = m[r];
+            }
+        }
+        // each of the wave's F slots' G bits of the words of steps c0 .. c0 + nn - 1
+#pragma unroll
+        for (int f = 0; f < F; f++) {
+            const int si = wv * F + f, lt = c0 + lane, t = si * sstep + lt;
+            if (si < sg.G && lane < nn && (si == 0 || lt >= sg.warm) && t < T) {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const uint64_t w = uint64_t(klo[r]) | (uint64_t(khi[r]) << 32);
+                    rows[size_t(t) * R + r] = G == 64 ? w : (w >> (f * G)) & ((uint64_t(1) << (G & 63)) - 1);
+                }
+            }
+        }
+    }
+
+    ts(2);
+    // exchange and boundary checks: segment i's metrics after its warm-up against segment i - 1's
+    // final metrics, equal up to a constant (both at phase 0: index = location = state)
+    int32_t* xf = reinterpret_cast<int32_t*>(sm + sg.x_lds);
+    int32_t* xw = xf + sg.G * N;
+    uint32_t* okf = reinterpret_cast<uint32_t*>(xw + sg.G * N);
+    if (seg < sg.G) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            xf[seg * N + r * 64 + int(l0)] = m[r];
+            xw[seg * N + r * 64 + int(l0)] = mw[r];
+        }
+    }
+    __syncthreads();
+    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
+    {
+        bool same = true;
+        if (seg >= 1 && seg < sg.G) {
+            const int d0 = xf[(seg - 1) * N] - xw[seg * N];  // state 0
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int d = r * 64 + int(l0);
+                same = same && xf[(seg - 1) * N + d] - xw[seg * N + d] == d0;
+            }
+        }
+        const bool ok = (__ballot(same) & fmask) == fmask;
+        if (lam == 0 && seg < sg.G) okf[seg] = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    if (wv != 0) return;  // (no barrier follows)
+    ts(3);
+    bool all = true;
+    for (int i = 0; i < sg.G; i++) all = all && okf[i] != 0u;
+    if (!all) {
+        if (sg.done && lane == 0) __hip_atomic_store(sg.done, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+
+    // ---- traceback, wave 0: 64 blocks of tbb steps over [0, T), lane b = block b ----
+    // (the global phase of a step is its local one: g_i = 0 mod S)
+    auto row = [&](int t, uint64_t (&w)[R], unsigned& sb) {
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r] = rows[size_t(t) * R + r];
+        sb = 0u;
+    };
+    constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
+    auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {  // the location before steps [lo, hi)
+        int t = hi, b = info_bit_pos<S>(hi - 1);
+        for (; t - kTb >= lo; t -= kTb) {
+            uint64_t w[kTb][R];
+            unsigned sb[kTb];
+#pragma unroll
+            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j], sb[j]);
+#pragma unroll
+            for (int j = 0; j < kTb; j++) {
+                loc = tb_step<S, R>(loc, w[j], b, sb[j]);
+                b = next_pos<S>(b);
+            }
+        }
+        for (; t > lo; t--) {
+            uint64_t w[R];
+            unsigned sb;
+            row(t - 1, w, sb);
+            loc = tb_step<S, R>(loc, w, b, sb);
+            b = next_pos<S>(b);
+        }
+        return loc;
+    };
+    constexpr int kWarm = 8 * S + 48;
+    const int tbb = ((T + 63) / 64 + 7) / 8 * 8;
+    const int lo = lane * tbb, top = lo + tbb < T ? lo + tbb : T;
+    const bool active = lo < T;
+    const int start = top + kWarm < T ? top + kWarm : T;
+    unsigned st = active ? walk(0u, start, top) : 0u;
+    unsigned s_top = st;
+    if (active) st = walk(st, top, lo);
+    unsigned fin = st;
+    bool fixed = !active || start == T;
+    // (one chain of up to 64 blocks: at most 63 re-walk rounds.)  Completeness guard: a block
+    // still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) sends the
+    // frame to lane 0's serial walk from state 0 at T (the reference's walk, :200-256)
+    const bool tbforce = (table.dbg & kDbgTbCap) != 0;
+    const int rounds = tbforce ? 0 : 65;
+    bool unproven = false;
+    for (int round = 0;; round++) {
+        const unsigned sf = unsigned(__shfl_down(int(fin), 1));
+        const bool ok = fixed || (s_top == sf && !tbforce);
+        const uint64_t bad = ~__ballot(ok);
+        if (bad == 0) break;
+        if (round == rounds) {
+            unproven = true;
+            break;
+        }
+        if (!ok && (bad >> (lane + 1)) == 0) {
+            s_top = sf;
+            fin = walk(sf, top, lo);
+            fixed = true;
+        }
+    }
+    int elo = lo, etop = top;
+    bool emit = active;
+    if (unproven) {
+        emit = lane == 0, elo = 0, etop = T, s_top = 0;
+        if (lane == 0) note_guard(table.guard_hits);
+    }
+    ts(4);
+    // the bytes into LDS (the input is no longer needed), MSB-first (reference :243-249)
+    uint8_t* ob = sm + sg.in_lds;
+    if (emit) {
+        unsigned byte = 0;
+        st = s_top;
+        int t = etop - 1, b = info_bit_pos<S>(etop - 1);
+        auto put = [&](int tt) {
+            if (tt < L) ob[tt >> 3] = uint8_t(tt + 8 > L ? byte & (0xffu << (tt + 8 - L)) : byte);
+        };
+        for (; t >= elo && ((t + 1) & 7) != 0; t--) {
+            byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
+            if ((t & 7) == 0) put(t);
+            uint64_t w[R];
+            unsigned sb;
+            row(t, w, sb);
+            st = tb_step<S, R>(st, w, b, sb);
+            b = next_pos<S>(b);
+        }
+        for (; t >= elo; t -= 8) {
+            uint64_t w[8][R];
+            unsigned sb[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) row(t - j, w[j], sb[j]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
+                st = tb_step<S, R>(st, w[j], b, sb[j]);
+                b = next_pos<S>(b);
+            }
+            put(t - 7);
+        }
+    }
+    ts(5);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int nbytes = (L + 7) >> 3;
+    if (((nbytes | int(size_t(out) & 3)) & 3) == 0) {
+        for (int i = lane; i < (nbytes >> 2); i += 64) reinterpret_cast<uint32_t*>(out)[i] = reinterpret_cast<const uint32_t*>(ob)[i];
+    } else {
+        for (int i = lane; i < nbytes; i += 64) out[i] = ob[i];
+    }
+    if (table.tstamp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ts(6);
+        if (threadIdx.x == 0) table.tstamp[7] = __builtin_amdgcn_s_memtime() - clk0;
+    }
+    if (sg.done) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(sg.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Segments and LDS of the single-frame path for S = a.S at `waves` waves and warm-up `warm`
+// (rounded up to whole loop bodies): the most segments (up to waves x F, at most kGenSegMax,
+// whose boundaries must all converge) that leave each at least kGenSegMin new steps.
+constexpr int kGenSegMin = 32;
+constexpr int kGenSegMax = 32;
+bool gen_seg_geometry(const Launch& a, int waves, int warm, GenSeg& g, size_t& lds) {
+    if (a.S < 2 || a.S > kMaxS || a.S == 6 || a.S == 8 || waves < 1 || waves > 8 || warm < 1) return false;
+    const int S = a.S, T = a.T, F = frames_per_wave(S), R = states_per_lane(S), N = 1 << S;
+    const int P = body_steps(S);
+    warm = (warm + P - 1) / P * P;
+    int G = waves * F;
+    if (G > kGenSegMax) G = kGenSegMax;
+    const int cap = (T - warm) / kGenSegMin;
+    if (G > cap) G = cap;
+    if (G < 2) return false;  // (too short to be worth segments: the batch kernel)
+    int sstep = (T - warm + G - 1) / G;
+    sstep = (sstep + P - 1) / P * P;
+    G = (T - warm + sstep - 1) / sstep;  // (the rounding may leave the last segments nothing to cover: dropped,
+    if (G < 2) return false;             // a segment past the frame would run on clamped input and need not converge)
+    const int n = sstep + warm;
+    if (G * sstep + warm < T) return false;
+    g.n = n, g.warm = warm, g.G = G, g.W = (G + F - 1) / F;
+    g.in_lds = (T * R * 8 + 15) / 16 * 16;
+    const int nin = (a.soft ? 2 : 1) * T;
+    g.x_lds = g.in_lds + (nin + 15) / 16 * 16;
+    lds = size_t(g.x_lds) + size_t(2 * G * N) * 4 + size_t(G) * 4;
+    return lds <= kLdsLimit && (T + 7) / 8 <= nin;
+}
+
+template <int S, bool SOFT>
+hipError_t launch_gen_seg_typed(const Launch& a, const GenSeg& g, size_t lds) {
+    auto kern = gen_seg_kernel<S, SOFT>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           int(lds));
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(64 * g.W), lds, a.stream, a.in, a.out, a.T, a.L, a, g);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+bool gen_seg_supported(const Launch& a, int waves, int warm) {
+    GenSeg g;
+    size_t lds = 0;
+    return gen_seg_geometry(a, waves, warm, g, lds);
+}
+
+hipError_t launch_gen_seg(const Launch& a, int waves, int warm, uint32_t* done) {
+    GenSeg g;
+    size_t lds = 0;
+    if (a.frames != 1 || !gen_seg_geometry(a, waves, warm, g, lds)) return hipErrorInvalidValue;
+    g.done = done;
+    note_kernel("gen_seg");
+    switch (a.S * 2 + (a.soft ? 1 : 0)) {
+        case 4: return launch_gen_seg_typed<2, false>(a, g, lds);
+        case 5: return launch_gen_seg_typed<2, true>(a, g, lds);
+        case 6: return launch_gen_seg_typed<3, false>(a, g, lds);
+        case 7: return launch_gen_seg_typed<3, true>(a, g, lds);
+        case 8: return launch_gen_seg_typed<4, false>(a, g, lds);
+        case 9: return launch_gen_seg_typed<4, true>(a, g, lds);
+        case 10: return launch_gen_seg_typed<5, false>(a, g, lds);
+        case 11: return launch_gen_seg_typed<5, true>(a, g, lds);
+        case 14: return launch_gen_seg_typed<7, false>(a, g, lds);
+        case 15: return launch_gen_seg_typed<7, true>(a, g, lds);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 bool lds_path_supported(const Launch& a) {
     // the GS variant takes every frame the LDS variant cannot hold
@@ -406,23 +926,17 @@ bool lds_path_supported(const Launch& a) {
 }
 
 // Which variant runs (measured on MI355X, 4,096-frame batches, K = 3..8 x L = 1,024..16,384,
-// tools/generic_sweep.py, profiles/r06/generic/sweep_r06c_batched_walk_noscratch.jsonl): GS, whose
-// waves need a few KB of LDS each (the CU holds every wave the batch gives it) and whose walks
-// load kTb steps' words at once, ran at or above the LDS variant everywhere (K = 4, L = 4,096
-// hard: 35.4 against 34.1 Gbit/s; K = 8, L = 4,096: 18.6 against 3.7, the LDS survivors cutting
-// the CU to one wave) except for K = 3 frames of 2,048+ steps, where a lane's walk covers T / 4
-// steps and the LDS variant fits the one wave per CU a 4,096-frame batch gives (L = 4,096 hard:
-// 27.6 against 26.1).  So: the LDS variant for K <= 4 frames of T >= 2,048 steps while it leaves
-// the CU the waves the batch needs, GS for everything else.
+// tools/generic_sweep.py): with the bpermute trellis (profiles/r06/generic/
+// sweep_r06c_batched_walk_noscratch.jsonl) the LDS variant won for K = 3, 4 frames of 2,048+ steps;
+// with the register-resident trellis and the prefetched staging (sweep_r06f_rot_pf.jsonl) GS runs
+// at or above it everywhere (K = 3, L = 4,096 hard: 48.3 against 34.5 Gbit/s; K = 4: 57.3 against
+// 45.9) -- the LDS survivors cap the waves per CU, GS's few KB do not.  So GS, and the LDS variant
+// only when VTB_DEBUG bit 20 asks for it (tests; it stays exact and selectable).
 bool lds_path_global(const Launch& a) {
     if (a.dbg & kDbgGenericGs) return true;
-    if (a.S >= 4 || a.T < 2048) return true;
+    if (!(a.dbg & kDbgGenericLds)) return true;
     const size_t w = bytes_per_wave(a.S, a.soft, a.T);
-    if (w == 0 || w > kLdsLimit) return true;
-    const size_t cus = a.cus > 0 ? (size_t)a.cus : 256;
-    size_t need = (gs_waves(a) + cus - 1) / cus;  // waves per CU the batch gives
-    if (need > 8) need = 8;
-    return kLdsLimit / w < need;
+    return w == 0 || w > kLdsLimit;
 }
 
 size_t lds_path_workspace_bytes(const Launch& a) {

@@ -98,14 +98,23 @@ def test_pure_noise_falls_back(orc, monkeypatch):
 
 @pytest.mark.parametrize("K", [3, 4, 5, 6, 8])
 @pytest.mark.parametrize("soft", [False, True])
-def test_other_k_frame_kernel(orc, K, soft, monkeypatch):
-    """K without a single-frame kernel of its own (the generic path, one frame per call), with
-    a generator pair of both end taps drawn at random per K."""
+def test_other_k_segments(orc, K, soft, monkeypatch):
+    """K without a single-frame kernel of its own: the generic kernel's segments (gen_seg_kernel,
+    round 6), with a generator pair of both end taps drawn at random per K.  Short frames (too few
+    steps for two segments) and frames whose segments' survivor words exceed the LDS take the batch
+    kernel; everything in between the segments, bit-exact either way (their use counted on a
+    standard code of each K)."""
     monkeypatch.delenv("VTB_KERNEL", raising=False)
     rng = np.random.default_rng(40 + K)
-    g = CODES[K] if K == 5 else tuple(int(1 | (1 << (K - 1)) | (int(rng.integers(0, 1 << K)) & ((1 << (K - 1)) - 2)))
-                                      for _ in range(2))
-    for L in (1, 77, 1000):
+    weak = tuple(int(1 | (1 << (K - 1)) | (int(rng.integers(0, 1 << K)) & ((1 << (K - 1)) - 2))) for _ in range(2))
+    std = {3: (0o7, 0o5), 4: (0o15, 0o17), 5: CODES[5], 6: (0o53, 0o75), 8: (0o247, 0o371)}[K]
+    # a random end-tapped pair (often a weak code, whose segments rarely converge: parity only)
+    for L in (1000,):
+        unc, rx = random_frames(orc, K, L, 3, 0.03, seed=K + L, g=weak)
+        d = ViterbiDecoder(ConvCode(K, weak), frame_bits=L)
+        assert (run(d, rx) == orc.decode(K, weak, rx, L)).all(), (K, weak, L)
+    g = std
+    for L in (1, 77, 200, 1000, 2048, 5001, 12000, 16384):
         if soft:
             unc, rx = random_frames(orc, K, L, 3, 0.0, seed=K + L, soft=True, sigma=0.6, g=g)
             rx = rx.reshape(3, -1)
@@ -114,7 +123,26 @@ def test_other_k_frame_kernel(orc, K, soft, monkeypatch):
         d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
         s0 = seg_stats()
         assert (run(d, rx) == orc.decode(K, g, rx, L, soft=soft)).all(), (K, g, L)
-        assert seg_stats()[2] - s0[2] == 3
+        ds = seg_stats() - s0
+        if L <= 77:
+            assert ds[2] == 3, (K, L, ds)  # no segments for so few steps
+        elif 1000 <= L <= 5001:
+            assert ds[0] >= 2, (K, L, ds)  # the segments decoded these frames
+            assert native.last_kernel() in ("gen_seg", "lds_path", "lds_path_gs")
+
+
+@pytest.mark.parametrize("K", [3, 5, 8])
+def test_other_k_pure_noise_falls_back(orc, K, monkeypatch):
+    """p = 0.5: the generic segments' metrics do not converge; the batch kernel decodes the frame
+    again, bit-exact."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    g = {3: (0o7, 0o5), 5: CODES[5], 8: (0o247, 0o371)}[K]
+    L = 2048
+    unc, rx = random_frames(orc, K, L, 6, 0.5, seed=7 + K, g=g)
+    d = ViterbiDecoder(ConvCode(K, g), frame_bits=L)
+    s0 = seg_stats()
+    assert (run(d, rx) == orc.decode(K, g, rx, L)).all()
+    assert seg_stats()[1] > s0[1]
 
 
 def test_k9_golden_vectors(monkeypatch):

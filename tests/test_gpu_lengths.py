@@ -31,6 +31,7 @@ from convolutionalencdec_amd import LIB_DIR, ConvCode, ViterbiDecoder, native  #
 
 SYMMETRIC = [n for n in sorted(LENGTH_CODES) if n != "k3"]
 GEN_GS = 1 << 19  # VTB_DEBUG: the generic kernel's global-survivor variant at every length
+GEN_LDS = 1 << 20  # VTB_DEBUG: the generic kernel's LDS variant wherever it fits one CU
 
 
 @pytest.fixture(scope="module")
@@ -46,7 +47,7 @@ def gpu_present():
 
 def _families(K):
     """(VTB_KERNEL, VTB_DEBUG) settings that decode constraint length K."""
-    fam = [(None, 0), ("lds", 0), ("lds", GEN_GS)]
+    fam = [(None, 0), ("lds", 0), ("lds", GEN_GS), ("lds", GEN_LDS)]
     if K == 7:
         fam += [("k7", 0), ("gws", 0), ("k7s", 0)]
     if K == 9:

@@ -36,7 +36,8 @@ NO_SPLIT = 1 << 8   # VTB_DEBUG: never split frames across the halves of a wave
 SEG_OFF = 1 << 10   # VTB_DEBUG: no single-frame SEG kernel
 K9_PAIR = 1 << 18   # VTB_DEBUG: K=9 frames on the pair kernel (not one frame per wave)
 GEN_GS = 1 << 19    # VTB_DEBUG: the generic kernel's global-survivor variant at every length
-GUARD_CODES = {**CODES, 3: (0o7, 0o5), 4: (0o15, 0o17)}
+GEN_LDS = 1 << 20   # VTB_DEBUG: the generic kernel's LDS variant wherever it fits
+GUARD_CODES = {**CODES, 3: (0o7, 0o5), 4: (0o15, 0o17), 6: (0o53, 0o75), 8: (0o247, 0o371)}
 
 
 @pytest.fixture(scope="module")
@@ -114,8 +115,10 @@ FRAME_CASES = [
     ("k9_soft", 9, 1024, 64, True, K9_PAIR, None, "k9"),
     ("k9_hard", 9, 1001, 33, False, K9_PAIR, None, "k9"),
     ("k9_loop", 9, 512, 24576, False, 0, None, "k9_loop"),
-    ("lds_path_k3", 3, 3000, 64, False, 0, None, "lds_path"),
-    ("lds_path_k4_soft", 4, 2500, 16, True, 0, None, "lds_path"),
+    ("lds_path_k3", 3, 3000, 64, False, GEN_LDS, None, "lds_path"),
+    ("lds_path_k4_soft", 4, 2500, 16, True, GEN_LDS, None, "lds_path"),
+    ("lds_path_k6", 6, 1000, 8, False, GEN_LDS, None, "lds_path"),
+    ("lds_path_k8_soft", 8, 600, 3, True, GEN_LDS, None, "lds_path"),
     ("lds_path_gs_k5", 5, 16384, 9, False, 0, None, "lds_path_gs"),
     ("lds_path_gs_k3", 3, 9000, 40, False, 0, None, "lds_path_gs"),
     ("lds_path_gs_k5_soft", 5, 3000, 17, True, GEN_GS, None, "lds_path_gs"),
@@ -143,7 +146,8 @@ def test_frame_kernels(orc, counter, monkeypatch, case, capped):
 
 
 @pytest.mark.parametrize("capped", [True, False], ids=["forced", "shipped"])
-@pytest.mark.parametrize("K,L,soft", [(7, 2048, True), (7, 3000, False), (9, 2048, True), (9, 1024, False)])
+@pytest.mark.parametrize("K,L,soft", [(7, 2048, True), (7, 3000, False), (9, 2048, True), (9, 1024, False),
+                                      (3, 3000, True), (5, 2048, False), (8, 2048, True)])
 def test_single_frame_seg(orc, counter, monkeypatch, K, L, soft, capped):
     """vtb_decode_frame_sync: the SEG kernels (one chain of up to 64 blocks over the frame's
     segments) and, where the segments do not converge, the frame kernels."""
@@ -151,17 +155,18 @@ def test_single_frame_seg(orc, counter, monkeypatch, K, L, soft, capped):
     # a spread of noise levels: the SEG kernel decodes a frame only if its segments' metrics
     # converge at every boundary, and its own guard fires only on such a frame whose traceback
     # blocks did not all verify on their first walk
+    g = GUARD_CODES[K]
     for i, (sigma, p) in enumerate(zip((0.7, 0.8, 0.9, 1.0, 1.1, 1.2, 1.3, 1.4, 1.6, 4.0),
                                        (0.05, 0.06, 0.07, 0.08, 0.09, 0.10, 0.11, 0.12, 0.14, 0.5))):
         if soft:
-            _, x = random_frames(orc, K, L, 2, 0.0, 40 + i, soft=True, sigma=sigma)
+            _, x = random_frames(orc, K, L, 2, 0.0, 40 + i, soft=True, sigma=sigma, g=g)
         else:
-            _, x = random_frames(orc, K, L, 2, p, 40 + i)
+            _, x = random_frames(orc, K, L, 2, p, 40 + i, g=g)
         frames.append(np.ascontiguousarray(x.reshape(2, -1)))
     x = np.concatenate(frames)
-    want = orc.decode(K, CODES[K], x, L, soft=soft, threads=16)
+    want = orc.decode(K, g, x, L, soft=soft, threads=16)
     _set_env(monkeypatch, CAP if capped else 0, None)
-    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
     got, seg_frames, seg_guarded = [], 0, 0
     for r in x:
         st0 = (ctypes.c_ulonglong * 3)()

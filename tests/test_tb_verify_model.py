@@ -124,7 +124,7 @@ def test_every_loop_cap_covers_its_chain():
     src9 = open(os.path.join(CSRC, "vtb_k9.hip")).read()
     assert "const int per = (Tq + 31) / 32;" in src9 and "const int per = (Tq + 63) / 64;" in src9
     assert _caps("vtb_genk.hip") == ["65"]  # one chain over the 64 lanes
-    assert _caps("vtb_lds_path.hip") == ["G + 1"]  # G lanes (blocks) per frame
+    assert _caps("vtb_lds_path.hip") == ["G + 1", "65"]  # G lanes (blocks) per frame; gen_seg: one chain of 64
     assert _caps("vtb_stream_gen.hip") == ["G + 1"]
 
 
