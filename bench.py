@@ -384,7 +384,7 @@ KERNEL_NOTES = {
     "k9_loop": "K=9 frame kernel, persistent over frame pairs, survivor words in a global workspace",
     "k9s": "K=9 one frame per wave64 (vtb_k9.hip k9s): 2 metric registers per lane, the frame's 256 locations in "
            "the u16 halves, survivor words in a global workspace",
-    "lds_path": "generic K=3..9 LDS kernel (vtb_lds_path.hip): int32 metrics, partners by ds_bpermute",
+    "lds_path": "generic K=3..9 kernel (vtb_lds_path.hip): int32 metrics in a register-resident trellis (DPP / permlane partners)",
 }
 
 
