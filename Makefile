@@ -13,7 +13,7 @@ CSRC := convolutionalencdec_amd/csrc
 
 HIP_SRCS := $(CSRC)/vtb_api.hip $(CSRC)/vtb_lds_path.hip $(CSRC)/vtb_k7_lds.hip $(CSRC)/vtb_k9.hip \
             $(CSRC)/vtb_gen.hip $(CSRC)/vtb_genk.hip $(CSRC)/vtb_legacy.hip $(CSRC)/vtb_stream_gen.hip
-HIP_HDRS := $(CSRC)/vtb_internal.h $(CSRC)/vtb_k7_common.h include/viterbi_amd.h
+HIP_HDRS := $(CSRC)/vtb_internal.h $(CSRC)/vtb_k7_common.h $(CSRC)/vtb_gen_trellis.h include/viterbi_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 
 LEGACY_SRCS := $(CSRC)/legacy/convEncode.c $(CSRC)/legacy/convHelpers.c $(CSRC)/legacy/viterbiDecoder.c

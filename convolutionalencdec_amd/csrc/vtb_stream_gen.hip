@@ -7,10 +7,11 @@
 // batch of streams advances in lockstep, one launch per call, and every stream emits the bits
 // that became final during the call:
 //   * ACS over the call's segments (all of them: no 48-step granularity, so no carry), one
-//     wave per F = 64 / G streams, state s of stream fi in lane fi*G + s % G, register s / G
-//     (vtb_lds_path.hip's layout and arithmetic: centred int32 metrics, strict '>' ties to the
-//     lower predecessor, :129-130), decisions as one ballot word per register per step into a
-//     per-wave survivor ring in global memory (step t at t mod W);
+//     wave per F = 64 / G streams on the register-resident trellis of vtb_gen_trellis.h
+//     (locations rotate with the step; centred int32 metrics, strict '>' ties to the lower
+//     predecessor, :129-130), decisions as one ballot word per register per step into a
+//     per-wave survivor ring in global memory (step t at t mod W, bit = lane of the location);
+//     a call may start at any phase (t_begin mod S), the metrics kept between calls by lane;
 //   * not last: walks from all N states at the call's end go back one step at a time until
 //     they stand on one state (step m); every survivor path passes through it, so no later
 //     input can change the bits below m: they equal the whole-frame decode's and are emitted
@@ -22,22 +23,17 @@
 // so a stream may run for any number of steps (< 2^30).  A stream that goes W steps without a
 // merge has lost survivors it still needs: it reports -1 until `last`, then restarts.
 
-#include "vtb_internal.h"
+#include "vtb_gen_trellis.h"
 
 namespace vtb {
 namespace {
 
+using namespace gen;
+
 template <int S>
-struct SGeo {
-    static constexpr int N = 1 << S;
-    static constexpr int G = N < 64 ? N : 64;  // lanes per stream
-    static constexpr int R = N / G;            // states per lane
-    static constexpr int F = 64 / G;           // streams per wave
-};
+using SGeo = Geometry<S>;
 
 constexpr int kStage = 64;  // steps of input staged into LDS per round
-
-__device__ __forceinline__ int bperm(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
 
 template <int S, bool SOFT>
 __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restrict__ in, size_t in_stride,
@@ -58,21 +54,16 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
     int32_t* st = state + size_t(blockIdx.x) * gen_stream_state_words(S);
     const int C = sa.t_end - sa.t_begin;  // steps of this call
 
-    // branch-metric coefficients of the lane's destinations (vtb_lds_path.hip)
-    int sig[R], kap[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int d = r * G + lam, c = table.symm[d >> 1], sb = (d & 1) ? -1 : 1;
-        const int s0 = ((c & 1) ? -1 : 1) * sb, s1 = ((c & 2) ? -1 : 1) * sb;
-        sig[r] = (s0 & 0xffff) | (s1 << 16);
-        kap[r] = (((c & 1) + ((c >> 1) & 1)) - 1) * Q * sb;
-    }
+    // the lane's trellis constants; metrics by location (the carried ones were stored by lane at
+    // the previous call's end, the same phase as this call's start)
+    const unsigned l0 = lane_of<S>(unsigned(lam));
+    Coef<S, R> coef;
+    setup_coef<S, R, Q>(table, l0, coef);
     int m[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) m[r] = sa.t_begin == 0 ? ((r * G + lam == 0) ? 0 : INIT) : st[r * 64 + lane];
+    for (int r = 0; r < R; r++) m[r] = sa.t_begin == 0 ? ((unsigned(r) * 64u + l0 == 0) ? 0 : INIT) : st[r * 64 + lane];
 
-    // ---- ACS over the call's steps ----
-    typedef short short2_t __attribute__((ext_vector_type(2)));
+    // ---- ACS over the call's steps (the phase of step t is t mod S, chosen per step) ----
     for (int c0 = 0; c0 < C; c0 += kStage) {
         const int n = C - c0 < kStage ? C - c0 : kStage;
         __syncthreads();
@@ -83,37 +74,15 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         __syncthreads();
         const uint8_t* my = sm + fi * kStage * SB;
         for (int i = 0; i < n; i++) {
-            int qp;
-            if constexpr (SOFT) {
-                qp = int(my[2 * i]) | (int(my[2 * i + 1]) << 16);
-            } else {
-                const int c = my[i];
-                qp = (c & 1) | (((c >> 1) & 1) << 16);
-            }
-            int nm[R];
+            const int t = sa.t_begin + c0 + i, ph = t % S;
+            const int qp = rx_pair<SOFT>(rx_raw<SOFT>(my + i * SB));
             uint64_t bal[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int l0 = fi * G + (r & 1) * (G / 2) + (lam >> 1);
-                int a0, a1;
-                if constexpr (R == 1) {
-                    a0 = bperm(m[0], l0);
-                    a1 = bperm(m[0], l0 + G / 2);
-                } else {
-                    a0 = bperm(m[r >> 1], l0);
-                    a1 = bperm(m[(r >> 1) + R / 2], l0);
-                }
-                const int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, sig[r]), __builtin_bit_cast(short2_t, qp),
-                                                      kap[r], false);
-                const int x0 = a0 + mu, x1 = a1 - mu;
-                const bool dd = x0 > x1;  // strict: ties keep the lower predecessor
-                nm[r] = dd ? x1 : x0;
-                bal[r] = __ballot(dd);
-            }
-#pragma unroll
-            for (int r = 0; r < R; r++) m[r] = nm[r];
+            gen_static_for(std::make_integer_sequence<int, S>{}, [&](auto pc) {
+                constexpr int PH = decltype(pc)::value;
+                if (ph == PH) rot_step<S, PH, R>(m, qp, coef, bal);
+            });
             if (lane == 0) {
-                const size_t slot = size_t((sa.t_begin + c0 + i) % W) * R;
+                const size_t slot = size_t(t % W) * R;
 #pragma unroll
                 for (int r = 0; r < R; r++) rg[slot + r] = bal[r];
             }
@@ -129,9 +98,11 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
     __threadfence_block();  // the ring words of this call before any walk reads them
     __syncthreads();
 
+    // the predecessor of state s after step t: the decision bit of s's location after step t
     auto pred = [&](unsigned s, int t) -> unsigned {
-        const uint64_t w = rg[size_t(t % W) * R + (s / G)];
-        return (s >> 1) | (unsigned((w >> (fi * G + (s % G))) & 1u) << (S - 1));
+        const unsigned loc = rotr_s<S>(s, (t + 1) % S);
+        const uint64_t w = rg[size_t(t % W) * R + (loc >> 6)];
+        return (s >> 1) | (unsigned((w >> (fi * G + lane_of<S>(loc & unsigned(G - 1)))) & 1u) << (S - 1));
     };
     const int e0 = st[64 * R + fi];
     const int flags = st[64 * R + 32 + fi];
