@@ -22,4 +22,14 @@ if [ "$2" = k9 ]; then  # the K=9 configuration (params/k9)
   grep -h "Rate" gpurun_out/speedDecode_ref_k9.log | tail -3 | sed 's/^/ref K=9: /'
   grep -h "Rate" gpurun_out/speedDecode_amd_k9.log | tail -3 | sed 's/^/amd K=9: /'
 fi
+if [ -n "$HARNESS_ALL" ]; then  # every other configuration the drop-in builds (params/<cfg>)
+  for c in k3s k4 k5 k6 k8; do
+    oracle/_ref/speedDecode_ref_$c > gpurun_out/speedDecode_ref_$c.log 2>&1 &
+    pid=$!; sleep $secs; kill $pid; wait $pid 2>/dev/null
+    oracle/_ref/speedDecode_amd_$c > gpurun_out/speedDecode_amd_$c.log 2>&1 &
+    pid=$!; sleep $((secs + 4)); kill $pid; wait $pid 2>/dev/null
+    grep -h "Rate" gpurun_out/speedDecode_ref_$c.log | tail -3 | sed "s/^/ref $c: /"
+    grep -h "Rate" gpurun_out/speedDecode_amd_$c.log | tail -3 | sed "s/^/amd $c: /"
+  done
+fi
 exit 0
