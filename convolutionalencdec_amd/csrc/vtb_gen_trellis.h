@@ -216,6 +216,13 @@ __device__ __forceinline__ unsigned tb_step(unsigned loc, const uint64_t (&w)[R]
 }
 
 
+// Traceback warm-up of a block walk (steps walked from a guessed state past the block's end):
+// survivor paths merge within a few constraint lengths, and a walk that entered on the wrong
+// state is caught by the chain verification and re-walked, so this only trades walk length
+// against re-walk rounds.
+template <int S>
+constexpr int kTbWarm = 4 * S + 24;
+
 // rotate right within S bits (k in [0, S)): the location of state x after a step of phase k - 1
 template <int S>
 __device__ __forceinline__ unsigned rotr_s(unsigned x, int k) {

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     // in state 0 there (exact when that is T, the terminated end), and a block is right once it
     // entered on its successor's exit location and that successor is proven; failed blocks re-walk
     // from a proven successor until all are.  Walks carry locations (state 0 is location 0).
-    constexpr int kWarm = 8 * S + 48;
+    constexpr int kWarm = kTbWarm<S>;
     // A step's R survivor words do not depend on the walk's location (only the bit taken from them
     // does), so the walks load kTb steps' words at once and then take the kTb dependent steps:
     // kTb loads in flight instead of one (GS: L2 / HBM latency; LDS: ds_read latency).
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
         }
         return loc;
     };
-    constexpr int kWarm = 8 * S + 48;
+    constexpr int kWarm = kTbWarm<S>;
     const int tbb = ((T + 63) / 64 + 7) / 8 * 8;
     const int lo = lane * tbb, top = lo + tbb < T ? lo + tbb : T;
     const bool active = lo < T;

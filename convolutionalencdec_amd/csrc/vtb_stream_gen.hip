@@ -63,9 +63,26 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
 #pragma unroll
     for (int r = 0; r < R; r++) m[r] = sa.t_begin == 0 ? ((unsigned(r) * 64u + l0 == 0) ? 0 : INIT) : st[r * 64 + lane];
 
-    // ---- ACS over the call's steps (the phase of step t is t mod S, chosen per step) ----
-    for (int c0 = 0; c0 < C; c0 += kStage) {
-        const int n = C - c0 < kStage ? C - c0 : kStage;
+    // ---- ACS over the call's steps ----
+    // The call starts at phase t_begin mod S: a first chunk of the (S - phase) mod S steps up to
+    // phase 0, then chunks of kChunk steps (whole phase cycles) run as static-phase cycles with
+    // the next cycle's received pairs read ahead; the call's last partial cycle and the first
+    // chunk step one at a time, the phase chosen per step.  The lane owning chunk step i keeps
+    // its R decision words (v_writelane); one ring store per chunk.
+    constexpr int kChunk = S * (kStage / S);
+    uint32_t klo[R], khi[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) klo[r] = khi[r] = 0;
+    auto keep = [&](const uint64_t (&bal)[R], int i) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            klo[r] = uint32_t(vtb_writelane(int(uint32_t(bal[r])), i, int(klo[r])));
+            khi[r] = uint32_t(vtb_writelane(int(uint32_t(bal[r] >> 32)), i, int(khi[r])));
+        }
+    };
+    const int pro = (S - sa.t_begin % S) % S;
+    for (int c0 = 0; c0 < C;) {
+        const int n = c0 == 0 && pro > 0 ? (pro < C ? pro : C) : (C - c0 < kChunk ? C - c0 : kChunk);
         __syncthreads();
         for (int idx = lane; idx < F * n * SB; idx += 64) {
             const int f = idx / (n * SB), o = idx - f * (n * SB);
@@ -73,20 +90,41 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         }
         __syncthreads();
         const uint8_t* my = sm + fi * kStage * SB;
-        for (int i = 0; i < n; i++) {
-            const int t = sa.t_begin + c0 + i, ph = t % S;
+        int i = 0;
+        if ((sa.t_begin + c0) % S == 0 && n >= S) {
+            auto load_q = [&](int at, int (&q)[S]) {
+#pragma unroll
+                for (int ph = 0; ph < S; ph++) q[ph] = rx_raw<SOFT>(my + (at + ph) * SB);
+            };
+            const int ncyc = n / S * S;
+            int q[S];
+            load_q(0, q);
+#pragma unroll
+            for (int ph = 0; ph < S; ph++) q[ph] = rx_pair<SOFT>(q[ph]);
+            for (; i < ncyc; i += S) {
+                int qn[S];
+                load_q(i + S < ncyc ? i + S : i, qn);
+                acs_cycle<S, R>(m, q, coef, klo, khi, i);
+#pragma unroll
+                for (int ph = 0; ph < S; ph++) q[ph] = rx_pair<SOFT>(qn[ph]);
+            }
+        }
+        for (; i < n; i++) {
+            const int ph = (sa.t_begin + c0 + i) % S;
             const int qp = rx_pair<SOFT>(rx_raw<SOFT>(my + i * SB));
             uint64_t bal[R];
             gen_static_for(std::make_integer_sequence<int, S>{}, [&](auto pc) {
                 constexpr int PH = decltype(pc)::value;
                 if (ph == PH) rot_step<S, PH, R>(m, qp, coef, bal);
             });
-            if (lane == 0) {
-                const size_t slot = size_t(t % W) * R;
-#pragma unroll
-                for (int r = 0; r < R; r++) rg[slot + r] = bal[r];
-            }
+            keep(bal, i);
         }
+        if (lane < n) {
+            const size_t slot = size_t((sa.t_begin + c0 + lane) % W) * R;
+#pragma unroll
+            for (int r = 0; r < R; r++) rg[slot + r] = uint64_t(klo[r]) | (uint64_t(khi[r]) << 32);
+        }
+        c0 += n;
     }
     // renormalise against state 0 of the lane's stream, keep the metrics for the next call
     const int ref = __shfl(m[0], fi * G);
