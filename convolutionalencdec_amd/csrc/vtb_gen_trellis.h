@@ -83,10 +83,12 @@ __device__ __forceinline__ int partner(int m) {
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
-// Received pair of one step: the raw bytes (hard: one symbol byte, soft: two bytes), then as
-// the packed operand of v_dot2 (hard: the two bits, soft: the bytes).  The recursion converts a
-// cycle's raw bytes only after the previous cycle's steps, so that their LDS reads are waited for
-// there and not where they are issued.
+// Received pair of one step: the raw bytes (hard: one symbol byte, soft: two bytes), then the
+// branch-metric operand: soft, the packed bytes for v_dot2; hard, the symbol's bit offset (8 c)
+// into the location's table of the four branch metrics (v_bfe_i32 reads offset bits 4..0 only,
+// so the symbol's bits above its two are ignored, as the reference's ignore them).  The
+// recursion converts a cycle's raw bytes only after the previous cycle's steps, so that their LDS
+// reads are waited for there and not where they are issued.
 template <bool SOFT>
 __device__ __forceinline__ int rx_raw(const uint8_t* p) {
     if constexpr (SOFT) {
@@ -100,7 +102,7 @@ __device__ __forceinline__ int rx_pair(int raw) {
     if constexpr (SOFT) {
         return raw;
     } else {
-        return (raw & 1) | (((raw >> 1) & 1) << 16);
+        return raw << 3;
     }
 }
 
@@ -117,20 +119,32 @@ __device__ __forceinline__ void coefficients(const Launch& table, unsigned l, in
     kap = (((c & 1) + ((c >> 1) & 1)) - 1) * Q;
 }
 
-// The per-lane constants of the recursion, by register and phase: branch-metric coefficients and
-// up = -1 where the location holds the upper predecessor (location bit p = S-1-ph set), else 0.
-template <int S, int R>
+// The per-lane constants of the recursion, by register and phase: branch-metric coefficients (soft:
+// v_dot2 operands sig, kap; hard: sig holds the four metrics mu(c) = sig . (c & 1, c >> 1) + kap,
+// c = 0..3, as signed bytes -- one v_bfe_i32 per step instead of a v_dot2 and the copy of its
+// accumulator) and up = -1 where the location holds the upper predecessor (location bit
+// p = S-1-ph set), else 0.
+template <int S, int R, bool SOFT>
 struct Coef {
     int sig[R][S], kap[R][S], up[R][S];
 };
-template <int S, int R, int Q>
-__device__ __forceinline__ void setup_coef(const Launch& table, unsigned l0, Coef<S, R>& k) {
+template <int S, int R, bool SOFT>
+__device__ __forceinline__ void setup_coef(const Launch& table, unsigned l0, Coef<S, R, SOFT>& k) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const unsigned l = unsigned(r) * 64u + l0;
 #pragma unroll
         for (int ph = 0; ph < S; ph++) {
-            coefficients<S, Q>(table, l, ph, k.sig[r][ph], k.kap[r][ph]);
+            int sig, kap;
+            coefficients<S, SOFT ? 255 : 1>(table, l, ph, sig, kap);
+            if constexpr (SOFT) {
+                k.sig[r][ph] = sig, k.kap[r][ph] = kap;
+            } else {
+                const int s0 = int(short(sig & 0xffff)), s1 = sig >> 16;
+                unsigned tab = 0;
+                for (int c = 0; c < 4; c++) tab |= unsigned((s0 * (c & 1) + s1 * (c >> 1) + kap) & 0xff) << (8 * c);
+                k.sig[r][ph] = int(tab), k.kap[r][ph] = 0;
+            }
             k.up[r][ph] = ((l >> (S - 1 - ph)) & 1u) ? -1 : 0;
         }
     }
@@ -141,14 +155,19 @@ __device__ __forceinline__ void setup_coef(const Launch& table, unsigned l0, Coe
 // ((own - partner's) ^ up) > up, i.e. own > partner's where the location holds the lower
 // predecessor and partner's > own where it holds the upper (tools/probes/genstep_probe.hip: 12 %
 // fewer cycles per step than two compares combined with the upper-lane mask on the SALU).
-template <int S, int PH, int R>
-__device__ __forceinline__ void rot_step(int (&m)[R], int qp, const Coef<S, R>& k, uint64_t (&bal)[R]) {
+template <int S, int PH, int R, bool SOFT>
+__device__ __forceinline__ void rot_step(int (&m)[R], int qp, const Coef<S, R, SOFT>& k, uint64_t (&bal)[R]) {
     constexpr int P = S - 1 - PH;
     int nm[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        const int mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, k.sig[r][PH]), __builtin_bit_cast(short2_t, qp),
-                                              k.kap[r][PH], false);
+        int mu;
+        if constexpr (SOFT) {
+            mu = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, k.sig[r][PH]), __builtin_bit_cast(short2_t, qp),
+                                        k.kap[r][PH], false);
+        } else {
+            mu = __builtin_amdgcn_sbfe(k.sig[r][PH], unsigned(qp), 8u);
+        }
         int pm;
         if constexpr (P >= 6) {
             pm = m[r ^ (1 << (P - 6))];
@@ -171,13 +190,13 @@ __device__ __forceinline__ void rot_step(int (&m)[R], int qp, const Coef<S, R>& 
 
 // One phase cycle (S steps) from the prepared received pairs q, the decision words kept by lanes
 // i .. i + S - 1 of klo / khi (v_writelane).
-template <int S, int R>
-__device__ __forceinline__ void acs_cycle(int (&m)[R], const int* q, const Coef<S, R>& k, uint32_t (&klo)[R],
+template <int S, int R, bool SOFT>
+__device__ __forceinline__ void acs_cycle(int (&m)[R], const int* q, const Coef<S, R, SOFT>& k, uint32_t (&klo)[R],
                                           uint32_t (&khi)[R], int i) {
     gen_static_for(std::make_integer_sequence<int, S>{}, [&](auto pc) {
         constexpr int PH = decltype(pc)::value;
         uint64_t bal[R];
-        rot_step<S, PH, R>(m, q[PH], k, bal);
+        rot_step<S, PH, R, SOFT>(m, q[PH], k, bal);
 #pragma unroll
         for (int r = 0; r < R; r++) {
             klo[r] = uint32_t(vtb_writelane(int(uint32_t(bal[r])), i + PH, int(klo[r])));

@@ -64,8 +64,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     const bool valid = myframe < frames;
 
     const unsigned l0 = lane_of<S>(unsigned(lam));  // this lane's location (register 0)
-    Coef<S, R> coef;
-    setup_coef<S, R, Q>(table, l0, coef);
+    Coef<S, R, SOFT> coef;
+    setup_coef<S, R, SOFT>(table, l0, coef);
     int m[R];
 #pragma unroll
     for (int r = 0; r < R; r++) m[r] = unsigned(r) * 64u + l0 == 0 ? 0 : INIT;  // phase 0: location = state
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
             int qn[P];
             load_q(base + (i + P < n ? i + P : i) * B, qn);
 #pragma unroll
-            for (int u = 0; u < U; u++) acs_cycle<S, R>(m, q + u * S, coef, klo, khi, i + u * S);
+            for (int u = 0; u < U; u++) acs_cycle<S, R, SOFT>(m, q + u * S, coef, klo, khi, i + u * S);
 #pragma unroll
             for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(qn[j]);
         }
@@ -186,13 +186,48 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         }
         return loc;
     };
+    // Emission while walking a block (MSB-first bytes, reference :243-249): bit t of the frame is
+    // the information bit of the location after step t; byte t / 8 is complete at step t = 0 mod 8
+    // (blocks start at multiples of 8).  A block first walked from a wrong entry writes wrong bytes;
+    // its re-walk, or the guard's serial walk, overwrites them later in program order -- so no
+    // separate emission walk.  The steps above the last whole octet one by one, then octets with
+    // their 8 rows loaded at once.
+    uint8_t* o = out + myframe * out_stride;
+    auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
+        unsigned byte = 0;
+        auto put = [&](int t) {
+            if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
+        };
+        int t = hi - 1, b = info_bit_pos<S>(hi - 1);
+        for (; t >= lo && ((t + 1) & 7) != 0; t--) {
+            byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+            if ((t & 7) == 0) put(t);
+            uint64_t w[R];
+            row(t, w);
+            loc = tb_step<S, R>(loc, w, b, fbase);
+            b = next_pos<S>(b);
+        }
+        for (; t >= lo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
+            uint64_t w[8][R];
+#pragma unroll
+            for (int j = 0; j < 8; j++) row(t - j, w[j]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+                loc = tb_step<S, R>(loc, w[j], b, fbase);
+                b = next_pos<S>(b);
+            }
+            put(t - 7);
+        }
+        return loc;
+    };
     const int tbb = ((T + G - 1) / G + 7) / 8 * 8;
     const int lo = lam * tbb, top = lo + tbb < T ? lo + tbb : T;
     const bool active = lo < T;
     const int start = top + kWarm < T ? top + kWarm : T;
     unsigned st = active ? walk(0u, start, top) : 0u;
     unsigned s_top = st;
-    if (active) st = walk(st, top, lo);
+    if (active) st = walk_emit(st, top, lo);
     unsigned fin = st;
     bool fixed = !active || start == T;
     const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
@@ -214,47 +249,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
         const uint64_t badf = (bad & fmask) >> (fi * G);  // this frame's failed blocks
         if (!ok && (badf >> (lam + 1)) == 0) {
             s_top = sf;
-            fin = walk(sf, top, lo);
+            fin = walk_emit(sf, top, lo);
             fixed = true;
         }
     }
-    int elo = lo, etop = top;  // emitted steps [elo, etop), from s_top after step etop - 1
-    bool emit = active;
-    if (unproven & fmask) {
-        emit = lam == 0, elo = 0, etop = T, s_top = 0;
-        if (lam == 0 && valid) note_guard(table.guard_hits);
-    }
-    if (!valid || !emit) return;
-    // Emission, MSB-first bytes (reference :243-249): bit t of the frame is the information bit
-    // of the location after step t; byte t / 8 is complete at step t = 0 mod 8 (elo is a
-    // multiple of 8).  The steps above the last whole octet of [elo, etop) one by one, then
-    // octets with their 8 rows loaded at once.
-    uint8_t* o = out + myframe * out_stride;
-    unsigned byte = 0;
-    st = s_top;
-    auto put = [&](int t) {
-        if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
-    };
-    int t = etop - 1, b = info_bit_pos<S>(etop - 1);
-    for (; t >= elo && ((t + 1) & 7) != 0; t--) {
-        byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
-        if ((t & 7) == 0) put(t);
-        uint64_t w[R];
-        row(t, w);
-        st = tb_step<S, R>(st, w, b, fbase);
-        b = next_pos<S>(b);
-    }
-    for (; t >= elo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
-        uint64_t w[8][R];
-#pragma unroll
-        for (int j = 0; j < 8; j++) row(t - j, w[j]);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
-            st = tb_step<S, R>(st, w[j], b, fbase);
-            b = next_pos<S>(b);
-        }
-        put(t - 7);
+    if ((unproven & fmask) && lam == 0) {
+        note_guard(table.guard_hits);
+        walk_emit(0u, T, 0);
     }
 }
 
@@ -397,8 +398,8 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
     const int fi = lane / G, lam = lane % G;
     // Measurement only (Launch::tstamp, tools/tstamp_seg.py): wave 0's phase times, 100 MHz
-    // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 4 chains proven,
-    // 5 bytes assembled, 6 output written; 7 = core clocks from 0 to 6
+    // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 4 blocks walked and
+    // emitted once, 5 chains proven (re-walks, guard), 6 output written; 7 = core clocks 0 to 6
     const uint64_t clk0 = table.tstamp ? __builtin_amdgcn_s_memtime() : 0;
     auto ts = [&](int k) {
         if (table.tstamp && threadIdx.x == 0) table.tstamp[k] = __builtin_amdgcn_s_memrealtime();
@@ -428,8 +429,8 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     const int sstep = sg.n - sg.warm;
     const int g0 = seg * sstep;  // a multiple of S
     const unsigned l0 = lane_of<S>(unsigned(lam));
-    Coef<S, R> coef;
-    setup_coef<S, R, Q>(table, l0, coef);
+    Coef<S, R, SOFT> coef;
+    setup_coef<S, R, SOFT>(table, l0, coef);
     int m[R], mw[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
             int qn[P];
             load_q(c0 + i + P, qn);
 #pragma unroll
-            for (int u = 0; u < U; u++) acs_cycle<S, R>(m, q + u * S, coef, klo, khi, i + u * S);
+            for (int u = 0; u < U; u++) acs_cycle<S, R, SOFT>(m, q + u * S, coef, klo, khi, i + u * S);
 #pragma unroll
             for (int j = 0; j < P; j++) q[j] = rx_pair<SOFT>(qn[j]);
             if (c0 + i + P == sg.warm) {
@@ -525,32 +526,59 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     }
 
     // ---- traceback, wave 0: 64 blocks of tbb steps over [0, T), lane b = block b ----
-    // (the global phase of a step is its local one: g_i = 0 mod S)
-    auto row = [&](int t, uint64_t (&w)[R], unsigned& sb) {
+    // (the global phase of a step is its local one: g_i = 0 mod S), the bytes into LDS (the input
+    // is no longer needed), emitted while walking as in lds_path_kernel
+    auto row = [&](int t, uint64_t (&w)[R]) {
 #pragma unroll
         for (int r = 0; r < R; r++) w[r] = rows[size_t(t) * R + r];
-        sb = 0u;
     };
     constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
     auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {  // the location before steps [lo, hi)
         int t = hi, b = info_bit_pos<S>(hi - 1);
         for (; t - kTb >= lo; t -= kTb) {
             uint64_t w[kTb][R];
-            unsigned sb[kTb];
 #pragma unroll
-            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j], sb[j]);
+            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
 #pragma unroll
             for (int j = 0; j < kTb; j++) {
-                loc = tb_step<S, R>(loc, w[j], b, sb[j]);
+                loc = tb_step<S, R>(loc, w[j], b, 0u);
                 b = next_pos<S>(b);
             }
         }
         for (; t > lo; t--) {
             uint64_t w[R];
-            unsigned sb;
-            row(t - 1, w, sb);
-            loc = tb_step<S, R>(loc, w, b, sb);
+            row(t - 1, w);
+            loc = tb_step<S, R>(loc, w, b, 0u);
             b = next_pos<S>(b);
+        }
+        return loc;
+    };
+    uint8_t* ob = sm + sg.in_lds;
+    auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
+        unsigned byte = 0;
+        auto put = [&](int tt) {
+            if (tt < L) ob[tt >> 3] = uint8_t(tt + 8 > L ? byte & (0xffu << (tt + 8 - L)) : byte);
+        };
+        int t = hi - 1, b = info_bit_pos<S>(hi - 1);
+        for (; t >= lo && ((t + 1) & 7) != 0; t--) {
+            byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+            if ((t & 7) == 0) put(t);
+            uint64_t w[R];
+            row(t, w);
+            loc = tb_step<S, R>(loc, w, b, 0u);
+            b = next_pos<S>(b);
+        }
+        for (; t >= lo; t -= 8) {
+            uint64_t w[8][R];
+#pragma unroll
+            for (int j = 0; j < 8; j++) row(t - j, w[j]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+                loc = tb_step<S, R>(loc, w[j], b, 0u);
+                b = next_pos<S>(b);
+            }
+            put(t - 7);
         }
         return loc;
     };
@@ -561,9 +589,10 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     const int start = top + kWarm < T ? top + kWarm : T;
     unsigned st = active ? walk(0u, start, top) : 0u;
     unsigned s_top = st;
-    if (active) st = walk(st, top, lo);
+    if (active) st = walk_emit(st, top, lo);
     unsigned fin = st;
     bool fixed = !active || start == T;
+    ts(4);
     // (one chain of up to 64 blocks: at most 63 re-walk rounds.)  Completeness guard: a block
     // still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) sends the
     // frame to lane 0's serial walk from state 0 at T (the reference's walk, :200-256)
@@ -581,48 +610,13 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
         }
         if (!ok && (bad >> (lane + 1)) == 0) {
             s_top = sf;
-            fin = walk(sf, top, lo);
+            fin = walk_emit(sf, top, lo);
             fixed = true;
         }
     }
-    int elo = lo, etop = top;
-    bool emit = active;
-    if (unproven) {
-        emit = lane == 0, elo = 0, etop = T, s_top = 0;
-        if (lane == 0) note_guard(table.guard_hits);
-    }
-    ts(4);
-    // the bytes into LDS (the input is no longer needed), MSB-first (reference :243-249)
-    uint8_t* ob = sm + sg.in_lds;
-    if (emit) {
-        unsigned byte = 0;
-        st = s_top;
-        int t = etop - 1, b = info_bit_pos<S>(etop - 1);
-        auto put = [&](int tt) {
-            if (tt < L) ob[tt >> 3] = uint8_t(tt + 8 > L ? byte & (0xffu << (tt + 8 - L)) : byte);
-        };
-        for (; t >= elo && ((t + 1) & 7) != 0; t--) {
-            byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
-            if ((t & 7) == 0) put(t);
-            uint64_t w[R];
-            unsigned sb;
-            row(t, w, sb);
-            st = tb_step<S, R>(st, w, b, sb);
-            b = next_pos<S>(b);
-        }
-        for (; t >= elo; t -= 8) {
-            uint64_t w[8][R];
-            unsigned sb[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) row(t - j, w[j], sb[j]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                byte = ((byte >> 1) | (((st >> b) & 1u) << 7)) & 0xffu;
-                st = tb_step<S, R>(st, w[j], b, sb[j]);
-                b = next_pos<S>(b);
-            }
-            put(t - 7);
-        }
+    if (unproven && lane == 0) {
+        note_guard(table.guard_hits);
+        walk_emit(0u, T, 0);
     }
     ts(5);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -645,17 +639,19 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
 }
 
 // Segments and LDS of the single-frame path for S = a.S at `waves` waves and warm-up `warm`
-// (rounded up to whole loop bodies): the most segments (up to waves x F, at most kGenSegMax,
-// whose boundaries must all converge) that leave each at least kGenSegMin new steps.
+// (rounded up to whole loop bodies): the most segments (up to waves x F, at most
+// gen_seg_max(S), whose boundaries must all converge) that leave each at least kGenSegMin new
+// steps.  K <= 4 codes forget their start within a few steps: 64 segments (K = 3 2,048-bit
+// frames: 80 steps per segment instead of 112); 32 above.
 constexpr int kGenSegMin = 32;
-constexpr int kGenSegMax = 32;
+constexpr int gen_seg_max(int S) { return S <= 3 ? 64 : 32; }
 bool gen_seg_geometry(const Launch& a, int waves, int warm, GenSeg& g, size_t& lds) {
     if (a.S < 2 || a.S > kMaxS || a.S == 6 || a.S == 8 || waves < 1 || waves > 8 || warm < 1) return false;
     const int S = a.S, T = a.T, F = frames_per_wave(S), R = states_per_lane(S), N = 1 << S;
     const int P = body_steps(S);
     warm = (warm + P - 1) / P * P;
     int G = waves * F;
-    if (G > kGenSegMax) G = kGenSegMax;
+    if (G > gen_seg_max(S)) G = gen_seg_max(S);
     const int cap = (T - warm) / kGenSegMin;
     if (G > cap) G = cap;
     if (G < 2) return false;  // (too short to be worth segments: the batch kernel)

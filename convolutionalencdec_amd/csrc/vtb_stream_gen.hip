@@ -57,8 +57,8 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
     // the lane's trellis constants; metrics by location (the carried ones were stored by lane at
     // the previous call's end, the same phase as this call's start)
     const unsigned l0 = lane_of<S>(unsigned(lam));
-    Coef<S, R> coef;
-    setup_coef<S, R, Q>(table, l0, coef);
+    Coef<S, R, SOFT> coef;
+    setup_coef<S, R, SOFT>(table, l0, coef);
     int m[R];
 #pragma unroll
     for (int r = 0; r < R; r++) m[r] = sa.t_begin == 0 ? ((unsigned(r) * 64u + l0 == 0) ? 0 : INIT) : st[r * 64 + lane];
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
             for (; i < ncyc; i += S) {
                 int qn[S];
                 load_q(i + S < ncyc ? i + S : i, qn);
-                acs_cycle<S, R>(m, q, coef, klo, khi, i);
+                acs_cycle<S, R, SOFT>(m, q, coef, klo, khi, i);
 #pragma unroll
                 for (int ph = 0; ph < S; ph++) q[ph] = rx_pair<SOFT>(qn[ph]);
             }
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
             uint64_t bal[R];
             gen_static_for(std::make_integer_sequence<int, S>{}, [&](auto pc) {
                 constexpr int PH = decltype(pc)::value;
-                if (ph == PH) rot_step<S, PH, R>(m, qp, coef, bal);
+                if (ph == PH) rot_step<S, PH, R, SOFT>(m, qp, coef, bal);
             });
             keep(bal, i);
         }

@@ -159,8 +159,9 @@ def body_steps(S):
     return 4 * S if S <= 2 else 2 * S if S <= 4 else S
 
 
-def gen_seg_geometry(S, T, waves, warm, seg_min=32, seg_max=32):
+def gen_seg_geometry(S, T, waves, warm, seg_min=32):
     """vtb_lds_path.hip gen_seg_geometry without the LDS check: (n, warm, G) or None."""
+    seg_max = 64 if S <= 3 else 32
     F = 64 >> S if S < 6 else 1
     P = body_steps(S)
     warm = (warm + P - 1) // P * P
@@ -238,3 +239,27 @@ def test_segment_geometry_never_leaves_a_segment_past_the_frame():
             n, warm, G = geo
             sstep = n - warm
             assert (G - 1) * sstep + warm < T and G * sstep + warm >= T, (S, T, geo)
+
+
+def sbfe8(word, offset):
+    """v_bfe_i32(word, offset, 8): offset bits 4..0 only, sign-extended byte."""
+    v = (word >> (offset & 31)) & 0xFF
+    return v - 256 if v >= 128 else v
+
+
+@pytest.mark.parametrize("K", [3, 4, 5, 6, 7, 8, 9])
+def test_hard_metric_table_matches_dot_form(K):
+    """Hard input: the kernels read a location's branch metric from a word of four signed bytes
+    (vtb_gen_trellis.h setup_coef, rot_step: v_bfe_i32 at offset 8 c, c the raw symbol byte
+    shifted by 3, whose bits above the symbol's two fall outside the offset's five bits) instead
+    of the v_dot2 form; every symbol byte gives the dot form's value of its two low bits."""
+    tr = Trellis(K, CODES[K], False)
+    for ph in range(tr.S):
+        for l in range(tr.N):
+            s0, s1, kap = int(tr.sig0[ph][l]), int(tr.sig1[ph][l]), int(tr.kap[ph][l])
+            tab = 0
+            for c in range(4):
+                tab |= ((s0 * (c & 1) + s1 * (c >> 1) + kap) & 0xFF) << (8 * c)
+            for raw in range(256):
+                want = s0 * (raw & 1) + s1 * ((raw >> 1) & 1) + kap
+                assert sbfe8(tab, raw << 3) == want, (K, ph, l, raw)

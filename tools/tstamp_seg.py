@@ -3,8 +3,8 @@ Launch::tstamp) on one frame decoded through vtb_decode_frame_sync.
 
     python tools/tstamp_seg.py [--K 3,4,5,6,8] [--frame-bits 2048] [--reps 50] [--soft]
 
-Per K: median microseconds of each phase (staging, steps, boundary checks, traceback chains,
-byte assembly, output) and the core clock (GHz) over the kernel.
+Per K: median microseconds of each phase (staging, steps, boundary checks, the block walks with
+their bytes, the chain verification, output) and the core clock (GHz) over the kernel.
 """
 import argparse
 import ctypes
@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-PHASES = ("stage", "steps", "check", "chains", "bytes", "output")
+PHASES = ("stage", "steps", "check", "walks", "verify", "output")
 
 
 def main():
