@@ -242,6 +242,114 @@ __device__ __forceinline__ unsigned tb_step(unsigned loc, const uint64_t (&w)[R]
 template <int S>
 constexpr int kTbWarm = 4 * S + 24;
 
+// Terminated traceback from state 0 (reference viterbiDecoderButterflyk1.c:200-256) of one frame
+// per chain of GC lanes, block-parallel and verified: chain ci = lane / GC,
+// block bi = lane % GC of tbb steps (a multiple of 8: every block owns whole output bytes).  A
+// block walks back to itself from kTbWarm steps past its end starting in location 0 there (exact
+// when that is T, the terminated end), writing its bytes (MSB-first, reference :243-249) as it
+// walks; it is right once it entered on its successor's exit location and that successor is
+// proven, and failed blocks re-walk (rewriting their bytes) from a proven successor until all are.
+// Chains of GC blocks need at most GC - 1 re-walk rounds.  Completeness guard: a chain with a
+// block still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is
+// walked again serially from location 0 at T by its block 0 (the reference's walk), whose bytes
+// overwrite the others' later in program order.  row(t, w) loads step t's R survivor words;
+// `base` is the frame's first bit in them; o the frame's output bytes (L bits); every lane of the
+// wave calls this (the chain checks are wave-wide).
+template <int S, int R, class Row>
+__device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned base, uint8_t* o, bool tbforce,
+                                                 uint32_t* guard_hits, Row&& row) {
+    constexpr int kWarm = kTbWarm<S>;
+    // A step's R survivor words do not depend on the walk's location (only the bit taken from them
+    // does), so the walks load kTb steps' words at once and then take the kTb dependent steps
+    // (kTb loads in flight instead of one: L2 / HBM or LDS latency).
+    constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
+    const int lane = int(threadIdx.x & 63), ci = lane / GC, bi = lane % GC;
+    // the location before steps [lo, hi) given the location after step hi - 1
+    auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {
+        int t = hi, b = info_bit_pos<S>(hi - 1);
+        for (; t - kTb >= lo; t -= kTb) {
+            uint64_t w[kTb][R];
+#pragma unroll
+            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
+#pragma unroll
+            for (int j = 0; j < kTb; j++) {
+                loc = tb_step<S, R>(loc, w[j], b, base);
+                b = next_pos<S>(b);
+            }
+        }
+        for (; t > lo; t--) {
+            uint64_t w[R];
+            row(t - 1, w);
+            loc = tb_step<S, R>(loc, w, b, base);
+            b = next_pos<S>(b);
+        }
+        return loc;
+    };
+    // the same walk, writing the bytes of [lo, hi) (lo a multiple of 8): the steps above the last
+    // whole octet one by one, then octets with their 8 rows loaded at once
+    auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
+        unsigned byte = 0;
+        auto put = [&](int t) {
+            if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
+        };
+        int t = hi - 1, b = info_bit_pos<S>(hi - 1);
+        for (; t >= lo && ((t + 1) & 7) != 0; t--) {
+            byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+            if ((t & 7) == 0) put(t);
+            uint64_t w[R];
+            row(t, w);
+            loc = tb_step<S, R>(loc, w, b, base);
+            b = next_pos<S>(b);
+        }
+        for (; t >= lo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
+            uint64_t w[8][R];
+#pragma unroll
+            for (int j = 0; j < 8; j++) row(t - j, w[j]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
+                loc = tb_step<S, R>(loc, w[j], b, base);
+                b = next_pos<S>(b);
+            }
+            put(t - 7);
+        }
+        return loc;
+    };
+    const int tbb = ((T + GC - 1) / GC + 7) / 8 * 8;
+    const int lo = bi * tbb, top = lo + tbb < T ? lo + tbb : T;
+    const bool active = lo < T;
+    const int start = top + kWarm < T ? top + kWarm : T;
+    unsigned st = active ? walk(0u, start, top) : 0u;
+    unsigned s_top = st;
+    if (active) st = walk_emit(st, top, lo);
+    unsigned fin = st;
+    bool fixed = !active || start == T;
+    const uint64_t cmask = (GC == 64 ? ~uint64_t(0) : ((uint64_t(1) << (GC & 63)) - 1)) << (ci * GC);
+    const int rounds = tbforce ? 0 : GC + 1;
+    const uint64_t live = __ballot(true);  // (lanes of frames past the batch have returned)
+    uint64_t unproven = 0;
+    for (int round = 0;; round++) {
+        const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry location
+        const bool ok = fixed || (s_top == sf && !tbforce);
+        const uint64_t bad = ~__ballot(ok) & live;
+        if (bad == 0) break;
+        if (round == rounds) {
+            unproven = bad;
+            break;
+        }
+        const uint64_t badc = (bad & cmask) >> (ci * GC);  // this chain's failed blocks
+        if (!ok && (badc >> (bi + 1)) == 0) {
+            s_top = sf;
+            fin = walk_emit(sf, top, lo);
+            fixed = true;
+        }
+    }
+    if ((unproven & cmask) && bi == 0) {
+        note_guard(guard_hits);
+        walk_emit(0u, T, 0);
+    }
+}
+
 // rotate right within S bits (k in [0, S)): the location of state x after a step of phase k - 1
 template <int S>
 __device__ __forceinline__ unsigned rotr_s(unsigned x, int k) {

@@ -149,114 +149,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     __syncthreads();
     if (!valid) return;
 
-    // Terminated traceback from state 0 (reference :200-256), block-parallel and verified
-    // (DESIGN.md §4.0): the frame's G lanes each take a block of tbb steps (a multiple of 8:
-    // every block owns whole output bytes), walk back to it from kWarm steps past its end starting
-    // in state 0 there (exact when that is T, the terminated end), and a block is right once it
-    // entered on its successor's exit location and that successor is proven; failed blocks re-walk
-    // from a proven successor until all are.  Walks carry locations (state 0 is location 0).
-    constexpr int kWarm = kTbWarm<S>;
-    // A step's R survivor words do not depend on the walk's location (only the bit taken from them
-    // does), so the walks load kTb steps' words at once and then take the kTb dependent steps:
-    // kTb loads in flight instead of one (GS: L2 / HBM latency; LDS: ds_read latency).
-    constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
-    const unsigned fbase = unsigned(fi * G);
-    auto row = [&](int t, uint64_t (&w)[R]) {
+    // the frame's G lanes trace it back (vtb_gen_trellis.h traceback_chains)
+    traceback_chains<S, R>(T, L, G, unsigned(fi * G), out + myframe * out_stride, (table.dbg & kDbgTbCap) != 0,
+                           table.guard_hits, [&](int t, uint64_t (&w)[R]) {
 #pragma unroll
-        for (int r = 0; r < R; r++) w[r] = dec[(size_t)t * R + r];
-    };
-    // the location before steps [lo, hi) given the location after step hi - 1
-    auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {
-        int t = hi, b = info_bit_pos<S>(hi - 1);
-        for (; t - kTb >= lo; t -= kTb) {
-            uint64_t w[kTb][R];
-#pragma unroll
-            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
-#pragma unroll
-            for (int j = 0; j < kTb; j++) {
-                loc = tb_step<S, R>(loc, w[j], b, fbase);
-                b = next_pos<S>(b);
-            }
-        }
-        for (; t > lo; t--) {
-            uint64_t w[R];
-            row(t - 1, w);
-            loc = tb_step<S, R>(loc, w, b, fbase);
-            b = next_pos<S>(b);
-        }
-        return loc;
-    };
-    // Emission while walking a block (MSB-first bytes, reference :243-249): bit t of the frame is
-    // the information bit of the location after step t; byte t / 8 is complete at step t = 0 mod 8
-    // (blocks start at multiples of 8).  A block first walked from a wrong entry writes wrong bytes;
-    // its re-walk, or the guard's serial walk, overwrites them later in program order -- so no
-    // separate emission walk.  The steps above the last whole octet one by one, then octets with
-    // their 8 rows loaded at once.
-    uint8_t* o = out + myframe * out_stride;
-    auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
-        unsigned byte = 0;
-        auto put = [&](int t) {
-            if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
-        };
-        int t = hi - 1, b = info_bit_pos<S>(hi - 1);
-        for (; t >= lo && ((t + 1) & 7) != 0; t--) {
-            byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
-            if ((t & 7) == 0) put(t);
-            uint64_t w[R];
-            row(t, w);
-            loc = tb_step<S, R>(loc, w, b, fbase);
-            b = next_pos<S>(b);
-        }
-        for (; t >= lo; t -= 8) {  // t = 7 mod 8: steps t .. t - 7
-            uint64_t w[8][R];
-#pragma unroll
-            for (int j = 0; j < 8; j++) row(t - j, w[j]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
-                loc = tb_step<S, R>(loc, w[j], b, fbase);
-                b = next_pos<S>(b);
-            }
-            put(t - 7);
-        }
-        return loc;
-    };
-    const int tbb = ((T + G - 1) / G + 7) / 8 * 8;
-    const int lo = lam * tbb, top = lo + tbb < T ? lo + tbb : T;
-    const bool active = lo < T;
-    const int start = top + kWarm < T ? top + kWarm : T;
-    unsigned st = active ? walk(0u, start, top) : 0u;
-    unsigned s_top = st;
-    if (active) st = walk_emit(st, top, lo);
-    unsigned fin = st;
-    bool fixed = !active || start == T;
-    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
-    // (chains of G blocks: at most G - 1 re-walk rounds.)  Completeness guard: a frame with a
-    // block still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is emitted by its lane 0
-    // alone, walking serially from state 0 at T (the reference's walk, :200-256)
-    const bool tbforce = (table.dbg & kDbgTbCap) != 0;
-    const int rounds = tbforce ? 0 : G + 1;
-    uint64_t unproven = 0;
-    for (int round = 0;; round++) {
-        const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry location
-        const bool ok = fixed || (s_top == sf && !tbforce);
-        const uint64_t bad = ~__ballot(ok);
-        if (bad == 0) break;
-        if (round == rounds) {
-            unproven = bad;
-            break;
-        }
-        const uint64_t badf = (bad & fmask) >> (fi * G);  // this frame's failed blocks
-        if (!ok && (badf >> (lam + 1)) == 0) {
-            s_top = sf;
-            fin = walk_emit(sf, top, lo);
-            fixed = true;
-        }
-    }
-    if ((unproven & fmask) && lam == 0) {
-        note_guard(table.guard_hits);
-        walk_emit(0u, T, 0);
-    }
+                               for (int r = 0; r < R; r++) w[r] = dec[(size_t)t * R + r];
+                           });
 }
 
 template <int S>
@@ -398,8 +296,8 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
     const int fi = lane / G, lam = lane % G;
     // Measurement only (Launch::tstamp, tools/tstamp_seg.py): wave 0's phase times, 100 MHz
-    // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 4 blocks walked and
-    // emitted once, 5 chains proven (re-walks, guard), 6 output written; 7 = core clocks 0 to 6
+    // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 5 traceback done,
+    // 6 output written; 7 = core clocks 0 to 6
     const uint64_t clk0 = table.tstamp ? __builtin_amdgcn_s_memtime() : 0;
     auto ts = [&](int k) {
         if (table.tstamp && threadIdx.x == 0) table.tstamp[k] = __builtin_amdgcn_s_memrealtime();
@@ -525,99 +423,14 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
         return;
     }
 
-    // ---- traceback, wave 0: 64 blocks of tbb steps over [0, T), lane b = block b ----
-    // (the global phase of a step is its local one: g_i = 0 mod S), the bytes into LDS (the input
-    // is no longer needed), emitted while walking as in lds_path_kernel
-    auto row = [&](int t, uint64_t (&w)[R]) {
-#pragma unroll
-        for (int r = 0; r < R; r++) w[r] = rows[size_t(t) * R + r];
-    };
-    constexpr int kTb = R == 1 ? 16 : R == 2 ? 8 : 4;
-    auto walk = [&](unsigned loc, int hi, int lo) -> unsigned {  // the location before steps [lo, hi)
-        int t = hi, b = info_bit_pos<S>(hi - 1);
-        for (; t - kTb >= lo; t -= kTb) {
-            uint64_t w[kTb][R];
-#pragma unroll
-            for (int j = 0; j < kTb; j++) row(t - 1 - j, w[j]);
-#pragma unroll
-            for (int j = 0; j < kTb; j++) {
-                loc = tb_step<S, R>(loc, w[j], b, 0u);
-                b = next_pos<S>(b);
-            }
-        }
-        for (; t > lo; t--) {
-            uint64_t w[R];
-            row(t - 1, w);
-            loc = tb_step<S, R>(loc, w, b, 0u);
-            b = next_pos<S>(b);
-        }
-        return loc;
-    };
+    // ---- traceback, wave 0: one chain of 64 blocks over [0, T) (the global phase of a step is
+    // its local one: g_i = 0 mod S), the bytes into LDS (the input is no longer needed) ----
     uint8_t* ob = sm + sg.in_lds;
-    auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
-        unsigned byte = 0;
-        auto put = [&](int tt) {
-            if (tt < L) ob[tt >> 3] = uint8_t(tt + 8 > L ? byte & (0xffu << (tt + 8 - L)) : byte);
-        };
-        int t = hi - 1, b = info_bit_pos<S>(hi - 1);
-        for (; t >= lo && ((t + 1) & 7) != 0; t--) {
-            byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
-            if ((t & 7) == 0) put(t);
-            uint64_t w[R];
-            row(t, w);
-            loc = tb_step<S, R>(loc, w, b, 0u);
-            b = next_pos<S>(b);
-        }
-        for (; t >= lo; t -= 8) {
-            uint64_t w[8][R];
+    traceback_chains<S, R>(T, L, 64, 0u, ob, (table.dbg & kDbgTbCap) != 0, table.guard_hits,
+                           [&](int t, uint64_t (&w)[R]) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) row(t - j, w[j]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                byte = ((byte >> 1) | (((loc >> b) & 1u) << 7)) & 0xffu;
-                loc = tb_step<S, R>(loc, w[j], b, 0u);
-                b = next_pos<S>(b);
-            }
-            put(t - 7);
-        }
-        return loc;
-    };
-    constexpr int kWarm = kTbWarm<S>;
-    const int tbb = ((T + 63) / 64 + 7) / 8 * 8;
-    const int lo = lane * tbb, top = lo + tbb < T ? lo + tbb : T;
-    const bool active = lo < T;
-    const int start = top + kWarm < T ? top + kWarm : T;
-    unsigned st = active ? walk(0u, start, top) : 0u;
-    unsigned s_top = st;
-    if (active) st = walk_emit(st, top, lo);
-    unsigned fin = st;
-    bool fixed = !active || start == T;
-    ts(4);
-    // (one chain of up to 64 blocks: at most 63 re-walk rounds.)  Completeness guard: a block
-    // still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) sends the
-    // frame to lane 0's serial walk from state 0 at T (the reference's walk, :200-256)
-    const bool tbforce = (table.dbg & kDbgTbCap) != 0;
-    const int rounds = tbforce ? 0 : 65;
-    bool unproven = false;
-    for (int round = 0;; round++) {
-        const unsigned sf = unsigned(__shfl_down(int(fin), 1));
-        const bool ok = fixed || (s_top == sf && !tbforce);
-        const uint64_t bad = ~__ballot(ok);
-        if (bad == 0) break;
-        if (round == rounds) {
-            unproven = true;
-            break;
-        }
-        if (!ok && (bad >> (lane + 1)) == 0) {
-            s_top = sf;
-            fin = walk_emit(sf, top, lo);
-            fixed = true;
-        }
-    }
-    if (unproven && lane == 0) {
-        note_guard(table.guard_hits);
-        walk_emit(0u, T, 0);
-    }
+                               for (int r = 0; r < R; r++) w[r] = rows[size_t(t) * R + r];
+                           });
     ts(5);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

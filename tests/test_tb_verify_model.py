@@ -93,7 +93,9 @@ def test_forced_guard_fires_on_every_walked_chain():
 def _caps(fname):
     src = open(os.path.join(CSRC, fname)).read()
     caps = re.findall(r"const int rounds = tbforce \? 0 : ([^;]+);", src)
-    assert len(re.findall(r"const bool tbforce = \((?:table\.|a\.)?dbg & kDbgTbCap\) != 0;", src)) == len(caps)
+    # (tbforce: VTB_DEBUG bit 17 read in the kernel, or passed in by it -- traceback_chains)
+    assert (len(re.findall(r"const bool tbforce = \((?:table\.|a\.)?dbg & kDbgTbCap\) != 0;", src))
+            + len(re.findall(r"\bbool tbforce,", src))) == len(caps)
     # bit 17 makes no check pass: the entry location poisoned (K=7 / K=9) or the check masked
     forced = (len(re.findall(r"if \(tbforce\) loc_top = ~0u;", src))
               + len(re.findall(r"const bool okb? = fixed \|\| \(\w+ == \w+ && !tbforce\);", src)))
@@ -124,11 +126,16 @@ def test_every_loop_cap_covers_its_chain():
     src9 = open(os.path.join(CSRC, "vtb_k9.hip")).read()
     assert "const int per = (Tq + 31) / 32;" in src9 and "const int per = (Tq + 63) / 64;" in src9
     assert _caps("vtb_genk.hip") == ["65"]  # one chain over the 64 lanes
-    assert _caps("vtb_lds_path.hip") == ["G + 1", "65"]  # G lanes (blocks) per frame; gen_seg: one chain of 64
+    # generic batch and single-frame kernels share traceback_chains: GC lanes (blocks) per chain,
+    # GC = G (lds_path_kernel) or 64 (gen_seg_kernel)
+    assert _caps("vtb_gen_trellis.h") == ["GC + 1"]
+    assert _caps("vtb_lds_path.hip") == []
+    src = open(os.path.join(CSRC, "vtb_lds_path.hip")).read()
+    assert src.count("traceback_chains<S, R>(T, L, G,") == 1 and src.count("traceback_chains<S, R>(T, L, 64,") == 1
     assert _caps("vtb_stream_gen.hip") == ["G + 1"]
 
 
-@pytest.mark.parametrize("fname", ["vtb_k7_lds.hip", "vtb_k9.hip", "vtb_genk.hip", "vtb_lds_path.hip",
+@pytest.mark.parametrize("fname", ["vtb_k7_lds.hip", "vtb_k9.hip", "vtb_genk.hip", "vtb_gen_trellis.h",
                                    "vtb_stream_gen.hip"])
 def test_every_guard_has_a_slow_path(fname):
     """After each loop an unproven chain reaches an exact slow path, and the testing counter

@@ -3,8 +3,9 @@ Launch::tstamp) on one frame decoded through vtb_decode_frame_sync.
 
     python tools/tstamp_seg.py [--K 3,4,5,6,8] [--frame-bits 2048] [--reps 50] [--soft]
 
-Per K: median microseconds of each phase (staging, steps, boundary checks, the block walks with
-their bytes, the chain verification, output) and the core clock (GHz) over the kernel.
+Per K: median microseconds of each phase (staging, steps, boundary checks (with the wait for the
+other waves), the verified traceback with its bytes, output) and the core clock (GHz) over the
+kernel.
 """
 import argparse
 import ctypes
@@ -18,7 +19,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-PHASES = ("stage", "steps", "check", "walks", "verify", "output")
+# (phase name, start entry, end entry) of the kernel's timestamps (gen_seg_kernel ts(k))
+PHASES = (("stage", 0, 1), ("steps", 1, 2), ("check", 2, 3), ("traceback", 3, 5), ("output", 5, 6))
 
 
 def main():
@@ -61,7 +63,7 @@ def main():
             print(json.dumps({"K": K, "note": "no gen_seg launch recorded", "kernel": native.last_kernel()}))
             continue
         b = np.array(rows)
-        ph = {n: float(np.median(b[:, i + 1] - b[:, i])) * 0.01 for i, n in enumerate(PHASES)}
+        ph = {n: float(np.median(b[:, j] - b[:, i])) * 0.01 for n, i, j in PHASES}
         ghz = float(np.median(b[:, 7] / np.maximum(b[:, 6] - b[:, 0], 1))) / 10.0
         print(json.dumps({"K": K, "L": a.frame_bits, "soft": a.soft, "n": len(rows),
                           "total_us": round(float(np.median(b[:, 6] - b[:, 0])) * 0.01, 2),
