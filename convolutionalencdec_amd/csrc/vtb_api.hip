@@ -55,11 +55,13 @@ struct vtb_plan {
     int seg9_wgs = 0;            // K = 9 SEG kernel workgroups (0: not usable for this plan)
     int seg9_waves = 0;          // and waves per workgroup
     int segg_waves = 0;          // generic SEG kernel (K = 3..6, 8) waves (0: not usable for this plan)
+    int segg_wgs = 0;            // and workgroups (> 1: its workspace in seg9_ws)
     // adaptive SEG warm-up (vtb_decode_frame_sync): the short warm-up while frames converge
     // with it; after a miss, the plan's warm-up for `seg_backoff` calls (doubling per miss)
     bool seg_short = false;
     int seg_backoff = 0, seg_skip = 0;
-    void* seg9_ws = nullptr;     // its workspace (arrival counter, metrics, survivor words)
+    void* seg9_ws = nullptr;     // the K=9 (or several-workgroup generic) SEG kernel's workspace
+                                 // (arrival counter, metrics, survivor words)
 };
 
 // Streaming decoder (include/viterbi_amd.h "Streaming decode"): all streams advance in
@@ -392,6 +394,7 @@ Knobs read_knobs() {
     k.seg_warm = num("VTB_SEG_WARM", 0);
     k.seg_adapt = num("VTB_SEG_ADAPT", 1) != 0;
     k.seg9_wgs = num("VTB_SEG9_WGS", 0);
+    k.segg_wgs = num("VTB_SEGG_WGS", 0);
     k.seg9_waves = num("VTB_SEG9_WAVES", 0);
     k.seg9_xcd = num("VTB_SEG9_XCD", -1);
     return k;
@@ -1058,7 +1061,7 @@ static int lat_undo(vtb_plan_t* plan, int err) {
     if (plan->lat_done) (void)hipHostFree(plan->lat_done);
     plan->seg9_ws = nullptr;
     plan->seg9_wgs = plan->seg9_waves = 0;
-    plan->segg_waves = 0;
+    plan->segg_waves = plan->segg_wgs = 0;
     plan->lat_in = plan->lat_out = nullptr;
     plan->lat_done = nullptr;
     plan->lat_d_in = plan->lat_d_out = nullptr;
@@ -1127,12 +1130,29 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
             plan->seg9_waves = w9;
         }
         // every other K (3..6, 8): the generic kernel's segments, eight waves ($VTB_SEG_WAVES:
-        // measurement), the short warm-up first as above
+        // measurement), the short warm-up first as above; K = 6, 8 over kSegGenWgs workgroups
+        // (one workgroup's slots give 16 / 8 segments; $VTB_SEGG_WGS: measurement)
         if (any && !(kn.dbg & 1024) && plan->seg_waves == 0 && plan->seg9_wgs == 0) {
             const int wg = kn.seg_waves > 0 ? kn.seg_waves : 8;
-            if (vtb::gen_seg_supported(a, wg, warm)) {
+            int nwg = kn.segg_wgs > 0 ? kn.segg_wgs : (a.S >= 5 ? vtb::kSegGenWgs : 1);
+            if (nwg > 1 && !vtb::gen_seg_supported(a, wg, nwg, warm)) nwg = 1;
+            if (vtb::gen_seg_supported(a, wg, nwg, warm)) {
+                const bool sg_short = short_ok && vtb::gen_seg_supported(a, wg, nwg, vtb::kSegWarmShort);
+                if (nwg > 1) {
+                    const size_t wsb = std::max(vtb::gen_seg_workspace_bytes(a, wg, nwg, warm),
+                                                sg_short ? vtb::gen_seg_workspace_bytes(a, wg, nwg, vtb::kSegWarmShort)
+                                                         : size_t(0));
+                    if (hipMalloc(&plan->seg9_ws, wsb) != hipSuccess) {
+                        plan->seg9_ws = nullptr;
+                        return lat_undo(plan, VTB_ERR_NOMEM);
+                    }
+                    // (the arrival counter zeroed in stream order, as for K = 9 above)
+                    if (hipMemsetAsync(plan->seg9_ws, 0, 256, plan->stream) != hipSuccess)
+                        return lat_undo(plan, VTB_ERR_DEVICE);
+                }
                 plan->segg_waves = wg;
-                plan->seg_short = short_ok && vtb::gen_seg_supported(a, wg, vtb::kSegWarmShort);
+                plan->segg_wgs = nwg;
+                plan->seg_short = sg_short;
             }
         }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&plan->lat_d_in), plan->lat_in, 0) != hipSuccess ||
@@ -1171,7 +1191,9 @@ int vtb_decode_frame_sync(vtb_plan_t* plan, const uint8_t* h_in, uint8_t* h_out)
         if (plan->seg_waves > 0) {
             if (vtb::launch_k7_seg(a, plan->seg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
         } else if (plan->segg_waves > 0) {
-            if (vtb::launch_gen_seg(a, plan->segg_waves, warm, d_done) != hipSuccess) return VTB_ERR_DEVICE;
+            a.ws = plan->seg9_ws;
+            if (vtb::launch_gen_seg(a, plan->segg_waves, plan->segg_wgs, warm, d_done) != hipSuccess)
+                return VTB_ERR_DEVICE;
         } else {
             a.ws = plan->seg9_ws;
             if (vtb::launch_k9_seg(a, plan->seg9_waves, plan->seg9_wgs, warm, d_done) != hipSuccess)

@@ -110,6 +110,7 @@ struct Knobs {
                               //   kSegWarm with the adaptive short warm-up (VTB_SEG_ADAPT=0 turns that off)
     bool seg_adapt = true;    // $VTB_SEG_ADAPT != "0"
     int seg9_wgs = 0;         // $VTB_SEG9_WGS > 0: K=9 SEG workgroups; else kSeg9Wgs
+    int segg_wgs = 0;         // $VTB_SEGG_WGS > 0: generic SEG workgroups; else kSegGenWgs for K = 6, 8, 1 below
     int seg9_waves = 0;       // $VTB_SEG9_WAVES > 0: K=9 SEG waves per workgroup; else kSeg9Waves
     int seg9_xcd = -1;        // $VTB_SEG9_XCD == 0: K=9 SEG grid stride 1 (workgroups spread over the
                               //   XCDs); any other value or unset: stride 8 (one XCD, one L2)
@@ -144,11 +145,15 @@ bool lds_path_global(const Launch& a);
 size_t lds_path_workspace_bytes(const Launch& a);
 hipError_t launch_lds_path(const Launch& a);
 // The single-frame path of the generic kernel (gen_seg_kernel, K = 3..6 and 8): one frame
-// (Launch::frames = 1) from host-mapped memory as segments over `waves` waves of one workgroup,
-// warm-up `warm` steps, *done as for K=7's SEG kernel (1 decoded, 2 not converged: nothing
-// written).
-bool gen_seg_supported(const Launch& a, int waves, int warm);
-hipError_t launch_gen_seg(const Launch& a, int waves, int warm, uint32_t* done);
+// (Launch::frames = 1) from host-mapped memory as segments over `waves` waves of each of `nwg`
+// workgroups, warm-up `warm` steps, *done as for K=7's SEG kernel (1 decoded, 2 not converged:
+// nothing written).
+constexpr int kSegGenWgs = 4;
+bool gen_seg_supported(const Launch& a, int waves, int nwg, int warm);
+// several workgroups (nwg > 1): the workspace (arrival counter zeroed once, in stream order,
+// metrics, rows); 0 for the single-workgroup form
+size_t gen_seg_workspace_bytes(const Launch& a, int waves, int nwg, int warm);
+hipError_t launch_gen_seg(const Launch& a, int waves, int nwg, int warm, uint32_t* done);
 
 // K=7, survivors in LDS (vtb_k7_lds.hip): the fast path.
 bool k7_lds_supported(const Launch& a);

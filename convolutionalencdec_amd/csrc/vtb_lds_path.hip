@@ -274,12 +274,35 @@ hipError_t launch_soft(const Launch& a) {
 // written and *done = 2 (the host decodes the frame with the batch kernel).  Input from and
 // output to host-mapped memory, *done = 1 with a system-scope release at the end.
 struct GenSeg {
-    int n = 0, warm = 0, G = 0, W = 0;  // steps per segment, warm-up, segments, waves
+    int n = 0, warm = 0, G = 0, W = 0;  // steps per segment, warm-up, segments, waves per workgroup
     int in_lds = 0;                     // LDS byte offset of the staged input, later the decoded bytes
                                         // (the frame's survivor rows, T R 8 bytes, from offset 0)
     int x_lds = 0;                      // exchange: final metrics [G][N], warm-up metrics [G][N], ok [G]
     uint32_t* done = nullptr;           // completion word (host-mapped) or null
+    // several workgroups (nwg > 1): rows and metrics handed over in a workspace
+    int nwg = 1;
+    uint32_t* counter = nullptr;  // workgroups arrived; the last one resets it
+    int32_t* gmet = nullptr;      // final metrics [G][N], warm-up metrics [G][N]
+    uint64_t* grows = nullptr;    // the frame's survivor rows [T][R]
 };
+
+// Words handed from one workgroup to another inside a launch: global agent-scope relaxed
+// accesses, i.e. sc1 stores and loads that bypass the per-CU L1 (cdna_hip_programming.md
+// Guideline 16; vtb_k9.hip k9_seg_kernel)
+typedef __attribute__((address_space(1))) uint32_t gen_gu32;
+typedef __attribute__((address_space(1))) uint64_t gen_gu64;
+__device__ __forceinline__ void st_agent32(int32_t* p, int32_t v) {
+    __hip_atomic_store((gen_gu32*)(p), uint32_t(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_agent32(const int32_t* p) {
+    return int32_t(__hip_atomic_load((const gen_gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gen_gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+    return __hip_atomic_load((const gen_gu64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 constexpr int kGenSegStage = 4;  // 16-byte staging loads per thread issued before their stores (v0..v3)
 
@@ -293,14 +316,19 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     constexpr int B = SOFT ? 2 : 1;
     extern __shared__ uint64_t smem[];
     uint8_t* sm = reinterpret_cast<uint8_t*>(smem);
+    // several workgroups: all working ones on one XCD (grid stride 8, one L2 for the hand-over);
+    // the others return at once
+    const bool multi = sg.nwg > 1;
+    if (multi && (blockIdx.x & 7u)) return;
+    const int wg = multi ? int(blockIdx.x >> 3) : 0;
     const int wv = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
     const int fi = lane / G, lam = lane % G;
     // Measurement only (Launch::tstamp, tools/tstamp_seg.py): wave 0's phase times, 100 MHz
     // ticks: 0 entry, 1 input staged, 2 steps done, 3 boundaries checked, 5 traceback done,
     // 6 output written; 7 = core clocks 0 to 6
     const uint64_t clk0 = table.tstamp ? __builtin_amdgcn_s_memtime() : 0;
-    auto ts = [&](int k) {
-        if (table.tstamp && threadIdx.x == 0) table.tstamp[k] = __builtin_amdgcn_s_memrealtime();
+    auto ts = [&](int k) {  // (several workgroups: 0-2 from workgroup 0, the rest from the last to arrive)
+        if (table.tstamp && threadIdx.x == 0 && (k >= 3 || wg == 0)) table.tstamp[k] = __builtin_amdgcn_s_memrealtime();
     };
     ts(0);
 
@@ -323,7 +351,8 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     __syncthreads();
     ts(1);
 
-    const int seg = wv * F + fi;  // this slot's segment
+    const int gwv = wg * sg.W + wv;  // the wave's index over the workgroups
+    const int seg = gwv * F + fi;    // this slot's segment
     const int sstep = sg.n - sg.warm;
     const int g0 = seg * sstep;  // a multiple of S
     const unsigned l0 = lane_of<S>(unsigned(lam));
@@ -374,50 +403,132 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
         // each of the wave's F slots' G bits of the words of steps c0 .. c0 + nn - 1
 #pragma unroll
         for (int f = 0; f < F; f++) {
-            const int si = wv * F + f, lt = c0 + lane, t = si * sstep + lt;
+            const int si = gwv * F + f, lt = c0 + lane, t = si * sstep + lt;
             if (si < sg.G && lane < nn && (si == 0 || lt >= sg.warm) && t < T) {
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const uint64_t w = uint64_t(klo[r]) | (uint64_t(khi[r]) << 32);
-                    rows[size_t(t) * R + r] = G == 64 ? w : (w >> (f * G)) & ((uint64_t(1) << (G & 63)) - 1);
+                    const uint64_t v = G == 64 ? w : (w >> (f * G)) & ((uint64_t(1) << (G & 63)) - 1);
+                    if (multi) {
+                        st_agent64(sg.grows + size_t(t) * R + r, v);
+                    } else {
+                        rows[size_t(t) * R + r] = v;
+                    }
                 }
             }
         }
     }
 
     ts(2);
-    // exchange and boundary checks: segment i's metrics after its warm-up against segment i - 1's
-    // final metrics, equal up to a constant (both at phase 0: index = location = state)
+    // boundary checks: segment i's metrics after its warm-up against segment i - 1's final
+    // metrics, equal up to a constant (both at phase 0: index = location = state)
     int32_t* xf = reinterpret_cast<int32_t*>(sm + sg.x_lds);
     int32_t* xw = xf + sg.G * N;
     uint32_t* okf = reinterpret_cast<uint32_t*>(xw + sg.G * N);
-    if (seg < sg.G) {
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            xf[seg * N + r * 64 + int(l0)] = m[r];
-            xw[seg * N + r * 64 + int(l0)] = mw[r];
-        }
-    }
-    __syncthreads();
-    const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
-    {
-        bool same = true;
-        if (seg >= 1 && seg < sg.G) {
-            const int d0 = xf[(seg - 1) * N] - xw[seg * N];  // state 0
+    bool all = true;
+    if (!multi) {
+        // one workgroup: the vectors exchanged in LDS, one check per slot
+        if (seg < sg.G) {
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                const int d = r * 64 + int(l0);
-                same = same && xf[(seg - 1) * N + d] - xw[seg * N + d] == d0;
+                xf[seg * N + r * 64 + int(l0)] = m[r];
+                xw[seg * N + r * 64 + int(l0)] = mw[r];
             }
         }
-        const bool ok = (__ballot(same) & fmask) == fmask;
-        if (lam == 0 && seg < sg.G) okf[seg] = ok ? 1u : 0u;
+        __syncthreads();
+        const uint64_t fmask = (G == 64 ? ~uint64_t(0) : ((uint64_t(1) << (G & 63)) - 1)) << (fi * G);
+        {
+            bool same = true;
+            if (seg >= 1 && seg < sg.G) {
+                const int d0 = xf[(seg - 1) * N] - xw[seg * N];  // state 0
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int d = r * 64 + int(l0);
+                    same = same && xf[(seg - 1) * N + d] - xw[seg * N + d] == d0;
+                }
+            }
+            const bool ok = (__ballot(same) & fmask) == fmask;
+            if (lam == 0 && seg < sg.G) okf[seg] = ok ? 1u : 0u;
+        }
+        __syncthreads();
+        if (wv != 0) return;  // (no barrier follows)
+        for (int i = 0; i < sg.G; i++) all = all && okf[i] != 0u;
+    } else {
+        // several workgroups: the vectors and the rows go through the workspace (sc1 stores,
+        // drained before the barrier); the last workgroup to arrive (one atomic add per
+        // workgroup, nobody waits) copies the rows into its LDS and checks every boundary
+        if (seg < sg.G) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                st_agent32(sg.gmet + size_t(seg) * N + r * 64 + int(l0), m[r]);
+                st_agent32(sg.gmet + size_t(sg.G + seg) * N + r * 64 + int(l0), mw[r]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            okf[0] = __hip_atomic_fetch_add((gen_gu32*)(sg.counter), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                             uint32_t(sg.nwg - 1)
+                         ? 1u
+                         : 0u;
+        __syncthreads();
+        if (okf[0] == 0u) return;  // (the whole workgroup: no barrier follows for it)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (orders the loads after the election)
+        // (every load of the hand-over issued before any use: one L2 round trip in all -- the
+        // boundary metrics of up to kBw boundaries per wave, then the rows into LDS)
+        constexpr int kBw = 8;  // boundaries a wave checks at once
+        bool ok = true;
+        for (int i0 = 1 + wv; i0 < sg.G; i0 += kBw * sg.W) {
+            int dx[kBw][R];
+#pragma unroll
+            for (int k = 0; k < kBw; k++) {
+                const int i = i0 + k * sg.W;
+                const int32_t* pf = sg.gmet + size_t(i - 1) * N;     // segment i - 1: final
+                const int32_t* pw = sg.gmet + size_t(sg.G + i) * N;  // segment i: warm-up end
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int l = r * 64 + lane;
+                    dx[k][r] = i < sg.G && l < N ? ld_agent32(pf + l) - ld_agent32(pw + l) : 0;
+                }
+            }
+            if (i0 == 1 + wv) {  // (the first group's loads in flight: the rows too)
+                const int bd = int(blockDim.x), TR = T * R;
+                for (int k = int(threadIdx.x); k < TR; k += 4 * bd) {
+                    uint64_t v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[j] = k + j * bd < TR ? ld_agent64(sg.grows + k + j * bd) : 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (k + j * bd < TR) rows[k + j * bd] = v[j];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kBw; k++) {
+                const int d0 = __shfl(dx[k][0], 0);  // state 0
+                bool same = true;
+#pragma unroll
+                for (int r = 0; r < R; r++) same = same && (r * 64 + lane >= N || dx[k][r] == d0);
+                ok = ok && (i0 + k * sg.W >= sg.G || __ballot(!same) == 0);
+            }
+        }
+        if (1 + wv >= sg.G) {  // (a wave without boundaries still copies its share of the rows)
+            const int bd = int(blockDim.x), TR = T * R;
+            for (int k = int(threadIdx.x); k < TR; k += 4 * bd) {
+                uint64_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[j] = k + j * bd < TR ? ld_agent64(sg.grows + k + j * bd) : 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (k + j * bd < TR) rows[k + j * bd] = v[j];
+            }
+        }
+        if (lane == 0) okf[1 + wv] = ok ? 1u : 0u;
+        __syncthreads();
+        if (wv != 0) return;  // (no barrier follows)
+        for (int i = 0; i < sg.W; i++) all = all && okf[1 + i] != 0u;
+        if (lane == 0) __hip_atomic_store((gen_gu32*)(sg.counter), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    if (wv != 0) return;  // (no barrier follows)
     ts(3);
-    bool all = true;
-    for (int i = 0; i < sg.G; i++) all = all && okf[i] != 0u;
     if (!all) {
         if (sg.done && lane == 0) __hip_atomic_store(sg.done, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
@@ -451,20 +562,22 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
     }
 }
 
-// Segments and LDS of the single-frame path for S = a.S at `waves` waves and warm-up `warm`
-// (rounded up to whole loop bodies): the most segments (up to waves x F, at most
-// gen_seg_max(S), whose boundaries must all converge) that leave each at least kGenSegMin new
-// steps.  K <= 4 codes forget their start within a few steps: 64 segments (K = 3 2,048-bit
-// frames: 80 steps per segment instead of 112); 32 above.
+// Segments and LDS of the single-frame path for S = a.S at `waves` waves per workgroup, `nwg`
+// workgroups and warm-up `warm` (rounded up to whole loop bodies): the most segments (up to
+// nwg x waves x F, at most gen_seg_max, whose boundaries must all converge) that leave each at
+// least kGenSegMin new steps.  One workgroup: K <= 4 codes forget their start within a few
+// steps, 64 segments (K = 3 2,048-bit frames: 80 steps per segment instead of 112), 32 above.
+// Several workgroups (K = 6, 8: the slots of one workgroup give 16 / 8 segments): up to 64.
 constexpr int kGenSegMin = 32;
-constexpr int gen_seg_max(int S) { return S <= 3 ? 64 : 32; }
-bool gen_seg_geometry(const Launch& a, int waves, int warm, GenSeg& g, size_t& lds) {
-    if (a.S < 2 || a.S > kMaxS || a.S == 6 || a.S == 8 || waves < 1 || waves > 8 || warm < 1) return false;
+constexpr int gen_seg_max(int S, int nwg) { return nwg > 1 || S <= 3 ? 64 : 32; }
+bool gen_seg_geometry(const Launch& a, int waves, int nwg, int warm, GenSeg& g, size_t& lds) {
+    if (a.S < 2 || a.S > kMaxS || a.S == 6 || a.S == 8 || waves < 1 || waves > 8 || nwg < 1 || nwg > 8 || warm < 1)
+        return false;
     const int S = a.S, T = a.T, F = frames_per_wave(S), R = states_per_lane(S), N = 1 << S;
     const int P = body_steps(S);
     warm = (warm + P - 1) / P * P;
-    int G = waves * F;
-    if (G > gen_seg_max(S)) G = gen_seg_max(S);
+    int G = waves * F * nwg;
+    if (G > gen_seg_max(S, nwg)) G = gen_seg_max(S, nwg);
     const int cap = (T - warm) / kGenSegMin;
     if (G > cap) G = cap;
     if (G < 2) return false;  // (too short to be worth segments: the batch kernel)
@@ -474,12 +587,29 @@ bool gen_seg_geometry(const Launch& a, int waves, int warm, GenSeg& g, size_t& l
     if (G < 2) return false;             // a segment past the frame would run on clamped input and need not converge)
     const int n = sstep + warm;
     if (G * sstep + warm < T) return false;
-    g.n = n, g.warm = warm, g.G = G, g.W = (G + F - 1) / F;
+    const int tw = (G + F - 1) / F;  // waves the segments need
+    g.n = n, g.warm = warm, g.G = G;
+    if (nwg > 1) {
+        g.W = waves, g.nwg = (tw + waves - 1) / waves;
+        if (g.nwg < 2) return false;  // (one workgroup holds them: the single-workgroup form)
+    } else {
+        g.W = tw, g.nwg = 1;
+    }
     g.in_lds = (T * R * 8 + 15) / 16 * 16;
     const int nin = (a.soft ? 2 : 1) * T;
     g.x_lds = g.in_lds + (nin + 15) / 16 * 16;
-    lds = size_t(g.x_lds) + size_t(2 * G * N) * 4 + size_t(G) * 4;
-    return lds <= kLdsLimit && (T + 7) / 8 <= nin;
+    const size_t x = size_t(2 * G * N) * 4 + size_t(G) * 4;  // (several workgroups: 1 + W flags)
+    lds = size_t(g.x_lds) + (x > 36 ? x : 36);
+    if (lds > kLdsLimit || (T + 7) / 8 > nin) return false;
+    // several workgroups: more than half a CU's LDS each, so that no two share a CU's SIMDs
+    if (g.nwg > 1 && lds < kLdsLimit / 2 + 1024) lds = kLdsLimit / 2 + 1024;
+    return true;
+}
+
+// workspace of the several-workgroup form: arrival counter, metrics, the frame's rows
+size_t gen_seg_ws_bytes(const Launch& a, const GenSeg& g) {
+    const size_t N = size_t(1) << a.S;
+    return 256 + (size_t(2) * g.G * N * 4 + 255) / 256 * 256 + size_t(a.T) * states_per_lane(a.S) * 8;
 }
 
 template <int S, bool SOFT>
@@ -490,23 +620,40 @@ hipError_t launch_gen_seg_typed(const Launch& a, const GenSeg& g, size_t lds) {
                                            int(lds));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(1), dim3(64 * g.W), lds, a.stream, a.in, a.out, a.T, a.L, a, g);
+    // several workgroups: placed 8 apart (round-robin over the XCDs: all on one XCD)
+    const unsigned grid = g.nwg > 1 ? unsigned(8 * g.nwg) : 1u;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * g.W), lds, a.stream, a.in, a.out, a.T, a.L, a, g);
     return hipGetLastError();
 }
 
 }  // namespace
 
-bool gen_seg_supported(const Launch& a, int waves, int warm) {
+bool gen_seg_supported(const Launch& a, int waves, int nwg, int warm) {
     GenSeg g;
     size_t lds = 0;
-    return gen_seg_geometry(a, waves, warm, g, lds);
+    return gen_seg_geometry(a, waves, nwg, warm, g, lds);
 }
 
-hipError_t launch_gen_seg(const Launch& a, int waves, int warm, uint32_t* done) {
+size_t gen_seg_workspace_bytes(const Launch& a, int waves, int nwg, int warm) {
     GenSeg g;
     size_t lds = 0;
-    if (a.frames != 1 || !gen_seg_geometry(a, waves, warm, g, lds)) return hipErrorInvalidValue;
+    if (nwg < 2 || !gen_seg_geometry(a, waves, nwg, warm, g, lds)) return 0;
+    return gen_seg_ws_bytes(a, g);
+}
+
+hipError_t launch_gen_seg(const Launch& a, int waves, int nwg, int warm, uint32_t* done) {
+    GenSeg g;
+    size_t lds = 0;
+    if (a.frames != 1 || !gen_seg_geometry(a, waves, nwg, warm, g, lds)) return hipErrorInvalidValue;
     g.done = done;
+    if (g.nwg > 1) {
+        if (!a.ws) return hipErrorInvalidValue;
+        uint8_t* base = static_cast<uint8_t*>(a.ws);
+        const size_t N = size_t(1) << a.S;
+        g.counter = reinterpret_cast<uint32_t*>(base);
+        g.gmet = reinterpret_cast<int32_t*>(base + 256);
+        g.grows = reinterpret_cast<uint64_t*>(base + 256 + (size_t(2) * g.G * N * 4 + 255) / 256 * 256);
+    }
     note_kernel("gen_seg");
     switch (a.S * 2 + (a.soft ? 1 : 0)) {
         case 4: return launch_gen_seg_typed<2, false>(a, g, lds);

@@ -159,13 +159,13 @@ def body_steps(S):
     return 4 * S if S <= 2 else 2 * S if S <= 4 else S
 
 
-def gen_seg_geometry(S, T, waves, warm, seg_min=32):
+def gen_seg_geometry(S, T, waves, warm, nwg=1, seg_min=32):
     """vtb_lds_path.hip gen_seg_geometry without the LDS check: (n, warm, G) or None."""
-    seg_max = 64 if S <= 3 else 32
+    seg_max = 64 if nwg > 1 or S <= 3 else 32
     F = 64 >> S if S < 6 else 1
     P = body_steps(S)
     warm = (warm + P - 1) // P * P
-    G = min(waves * F, seg_max, (T - warm) // seg_min)
+    G = min(waves * F * nwg, seg_max, (T - warm) // seg_min)
     if G < 2:
         return None
     sstep = (T - warm + G - 1) // G
@@ -173,14 +173,16 @@ def gen_seg_geometry(S, T, waves, warm, seg_min=32):
     G = (T - warm + sstep - 1) // sstep
     if G < 2:
         return None
+    if nwg > 1 and (G + F - 1) // F <= waves:
+        return None  # (one workgroup holds them: the single-workgroup form)
     return sstep + warm, warm, G
 
 
-def decode_segments(tr, x, L, waves=8, warm=48):
+def decode_segments(tr, x, L, waves=8, warm=48, nwg=1):
     """The segment decode: None if a boundary did not converge (the kernel's *done = 2)."""
     S, N = tr.S, tr.N
     T = L + S
-    geo = gen_seg_geometry(S, T, waves, warm)
+    geo = gen_seg_geometry(S, T, waves, warm, nwg)
     assert geo is not None
     n, warm, G = geo
     sstep = n - warm
@@ -211,15 +213,17 @@ def decode_segments(tr, x, L, waves=8, warm=48):
     return traceback(tr, rows, T, L)
 
 
-@pytest.mark.parametrize("K,L", [(3, 1000), (3, 2048), (4, 1000), (5, 2048), (6, 1000), (8, 2048)])
-def test_segments_match_oracle_when_converged(orc, K, L):
+@pytest.mark.parametrize("K,L,nwg", [(3, 1000, 1), (3, 2048, 1), (4, 1000, 1), (5, 2048, 1), (6, 1000, 1),
+                                     (8, 2048, 1), (6, 2048, 4), (8, 2048, 4)])
+def test_segments_match_oracle_when_converged(orc, K, L, nwg):
+    """(nwg = 4: the shipped form for K = 6, 8 -- up to 64 segments over four workgroups.)"""
     g = CODES[K]
     unc, rx = random_frames(orc, K, L, 2, 0.02, seed=100 + K, g=g)
     want = orc.decode(K, g, rx, L)
     tr = Trellis(K, g, False)
     converged = 0
     for f in range(2):
-        got = decode_segments(tr, rx[f], L)
+        got = decode_segments(tr, rx[f], L, nwg=nwg)
         if got is not None:
             converged += 1
             assert (got == want[f]).all(), (K, L, f)
@@ -233,12 +237,13 @@ def test_segment_geometry_never_leaves_a_segment_past_the_frame():
         if S == 6:
             continue
         for T in range(80, 4200, 37):
-            geo = gen_seg_geometry(S, T, 8, 48)
-            if geo is None:
-                continue
-            n, warm, G = geo
-            sstep = n - warm
-            assert (G - 1) * sstep + warm < T and G * sstep + warm >= T, (S, T, geo)
+            for nwg in (1, 4):
+                geo = gen_seg_geometry(S, T, 8, 48, nwg)
+                if geo is None:
+                    continue
+                n, warm, G = geo
+                sstep = n - warm
+                assert (G - 1) * sstep + warm < T and G * sstep + warm >= T, (S, T, nwg, geo)
 
 
 def sbfe8(word, offset):

@@ -59,7 +59,7 @@ def test_env_read_only_in_read_knobs():
             body = src[src.index("Knobs read_knobs() {"):]
             body = body[:body.index("\n}\n")]
             for knob in ("VTB_DEBUG", "VTB_SPLIT_WARM", "VTB_GENK_WARM", "VTB_SEG_WAVES", "VTB_SEG_WARM",
-                         "VTB_SEG_ADAPT", "VTB_SEG9_WGS", "VTB_SEG9_WAVES", "VTB_SEG9_XCD"):
+                         "VTB_SEG_ADAPT", "VTB_SEG9_WGS", "VTB_SEG9_WAVES", "VTB_SEG9_XCD", "VTB_SEGG_WGS"):
                 assert f'num("{knob}"' in body, knob
         elif os.path.basename(path) == "vtb_legacy.hip":
             assert set(names) <= {"VTB_LEGACY_DEVICE"}, names
