@@ -187,6 +187,31 @@ def test_k9_workgroup_counts(orc, wgs, xcd, monkeypatch):
     assert (run(d, rx) == orc.decode(9, CODES[9], rx, L)).all()
 
 
+@pytest.mark.parametrize("soft", [False, True])
+@pytest.mark.parametrize("wgs", [1, 2, 4, 8])
+@pytest.mark.parametrize("K", [6, 8])
+def test_generic_segment_workgroups(orc, K, wgs, soft, monkeypatch):
+    """K = 6, 8 single frames: the generic segments on one workgroup (the LDS hand-over) and over
+    2, 4 (shipped) and 8 workgroups (the workspace hand-over, the last workgroup to arrive checks
+    and traces back), bit-exact against the oracle, and decoded by the segments."""
+    monkeypatch.delenv("VTB_KERNEL", raising=False)
+    monkeypatch.setenv("VTB_SEGG_WGS", str(wgs))
+    g = {6: (0o53, 0o75), 8: (0o247, 0o371)}[K]
+    for L in (1500, 2048, 4000):
+        if soft:
+            unc, rx = random_frames(orc, K, L, 3, 0.0, seed=K * wgs + L, soft=True, sigma=0.6, g=g)
+            rx = rx.reshape(3, -1)
+        else:
+            unc, rx = random_frames(orc, K, L, 3, 0.02, seed=K * wgs + L, g=g)
+        d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
+        s0 = seg_stats()
+        assert (run(d, rx) == orc.decode(K, g, rx, L, soft=soft)).all(), (K, wgs, L, soft)
+        ds = seg_stats() - s0
+        assert ds[0] >= 2 and ds[2] == 0, (K, wgs, L, soft, ds)
+        assert native.last_kernel() in ("gen_seg", "lds_path_gs"), native.last_kernel()
+        d.close()
+
+
 def test_k9_pure_noise_falls_back(orc, monkeypatch):
     monkeypatch.delenv("VTB_KERNEL", raising=False)
     L = 2048
