@@ -90,10 +90,12 @@ def test_random_case_vs_oracle(orc, case):
 
 
 def _frame_cases(n=FUZZ_N or 72, seed=(FUZZ_SEED + 1) if FUZZ_SEED else 20261017):
+    """K = 7, 9 (their SEG kernels) two cases in three; every other K (the generic segments,
+    round 6: K = 3..6 on one workgroup, K = 6, 8 over four) the third."""
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
-        K = 9 if i % 3 == 2 else 7
+        K = (7, 9, int(rng.choice([3, 4, 5, 6, 8])))[i % 3]
         soft = bool(rng.integers(0, 2))
         L = int(rng.integers(1, 4090 if soft else 8100))
         if K == 9 and L > 12000:
@@ -106,19 +108,20 @@ def _frame_cases(n=FUZZ_N or 72, seed=(FUZZ_SEED + 1) if FUZZ_SEED else 20261017
 @pytest.mark.parametrize("case", _frame_cases(),
                          ids=lambda c: f"{c[0]}-K{c[4]}-L{c[1]}-{'soft' if c[2] else 'hard'}-p{c[3]}")
 def test_single_frame_path_vs_oracle(orc, case, monkeypatch):
-    """vtb_decode_frame_sync (the segmented single-frame kernels, K=7 on one workgroup and K=9
-    over several, or the frame-kernel fallback when a segment has not converged) at random
-    frame lengths and noise levels."""
+    """vtb_decode_frame_sync (the segmented single-frame kernels, K=7 on one workgroup, K=9
+    over several, the generic segments for every other K, or the frame-kernel fallback when a
+    segment has not converged) at random frame lengths and noise levels."""
     monkeypatch.delenv("VTB_KERNEL", raising=False)
     i, L, soft, noise, K = case
+    g = FUZZ_CODES[K]
     if soft:
         sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
-        unc, x = random_frames(orc, K, L, 3, 0.0, 5000 + i, soft=True, sigma=sigma)
+        unc, x = random_frames(orc, K, L, 3, 0.0, 5000 + i, soft=True, sigma=sigma, g=g)
     else:
-        unc, x = random_frames(orc, K, L, 3, noise, 5000 + i)
+        unc, x = random_frames(orc, K, L, 3, noise, 5000 + i, g=g)
     x = np.ascontiguousarray(x).reshape(3, -1)
-    want = orc.decode(K, CODES[K], x, L, soft=soft, threads=THREADS)
-    d = ViterbiDecoder(ConvCode(K, CODES[K]), frame_bits=L, soft=soft)
+    want = orc.decode(K, g, x, L, soft=soft, threads=THREADS)
+    d = ViterbiDecoder(ConvCode(K, g), frame_bits=L, soft=soft)
     got = np.stack([d.decode_frame(r) for r in x])
     assert (got == want).all(), case
 
