@@ -143,7 +143,7 @@ def _stream_cases(n=(FUZZ_N // 8) or 24, seed=(FUZZ_SEED + 2) if FUZZ_SEED else 
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
-        K = int(rng.choice([7, 7, 9]))
+        K = int(rng.choice([7, 7, 9, 3, 4, 5, 6, 8]))  # (K != 7, 9: the generic stream kernel)
         soft = bool(rng.integers(0, 2))
         L = int(rng.integers(1, 6000))
         F = int(rng.integers(1, 10))
@@ -155,24 +155,25 @@ def _stream_cases(n=(FUZZ_N // 8) or 24, seed=(FUZZ_SEED + 2) if FUZZ_SEED else 
 @pytest.mark.parametrize("case", _stream_cases(),
                          ids=lambda c: f"{c[0]}-K{c[1]}-L{c[2]}-F{c[3]}-{'soft' if c[4] else 'hard'}-p{c[5]}")
 def test_stream_random_chunking_vs_oracle(orc, case):
-    """The streaming decoder (vtb_stream_*, K=7 and K=9) at random frame lengths, stream
-    counts, noise levels and chunkings (calls of 0 to 1,200 segments, two frames per object):
+    """The streaming decoder (vtb_stream_*: K=7, K=9 and the generic stream kernel, whose calls
+    start at any trellis phase) at random frame lengths, stream counts, noise levels and
+    chunkings (calls of 0 to 1,200 segments, two frames per object):
     the bits each stream emits over a frame's calls, concatenated, equal the oracle's
     whole-frame decode."""
     from convolutionalencdec_amd import ViterbiStream
 
     i, K, L, F, soft, noise = case
     rng = np.random.default_rng(4000 + i)
-    g = CODES[K]
+    g = FUZZ_CODES[K]
     sb = 2 if soft else 1
     T = L + K - 1
     vs = ViterbiStream(ConvCode(K, g), streams=F, soft=soft)
     for frame in range(2):
         if soft:
             sigma = {0.0: 0.3, 0.03: 0.56, 0.07: 0.7, 0.5: 4.0}[noise]
-            unc, x = random_frames(orc, K, L, F, 0.0, 3000 + 2 * i + frame, soft=True, sigma=sigma)
+            unc, x = random_frames(orc, K, L, F, 0.0, 3000 + 2 * i + frame, soft=True, sigma=sigma, g=g)
         else:
-            unc, x = random_frames(orc, K, L, F, noise, 3000 + 2 * i + frame)
+            unc, x = random_frames(orc, K, L, F, noise, 3000 + 2 * i + frame, g=g)
         x = np.ascontiguousarray(x).reshape(F, -1)
         want = np.unpackbits(orc.decode(K, g, x, L, soft=soft, threads=THREADS), axis=1)[:, :L]
         xd = torch.from_numpy(x).cuda()
