@@ -262,13 +262,16 @@ hipError_t launch_soft(const Launch& a) {
 // vtb_decode_frame_sync for the codes without a SEG kernel of their own (K = 3..6, 8; K = 7 and
 // K = 9 have k7_seg / k9_seg): one frame at a time is one dependent chain of T steps, so the frame
 // is cut into G segments decoded at once by the F = 64 / min(N, 64) frame slots of each of up to
-// eight waves of one workgroup (the batch kernel's trellis layout and arithmetic above).  Segment
+// eight waves of one workgroup -- or, for K = 6, 8, of several workgroups on one XCD whose rows and
+// metric vectors go through a workspace to the last one to arrive (vtb_k9.hip's hand-over) -- on
+// the batch kernel's trellis layout and arithmetic (vtb_gen_trellis.h).  Segment
 // i runs n steps from g_i = i (n - warm); segment 0 starts from the reference's start metrics,
 // the others from equal metrics.  Segment i's decisions are the frame's from s_i = g_i + warm on
 // when its metric vector there equals segment i - 1's final one up to a constant (the trellis
 // compares differences only; segment i - 1 is exact up to s_i by induction) -- vtb_k7_lds.hip's
-// SEG argument.  n and warm are whole loop bodies (P steps, a multiple of S: every g_i is one, all slots of a
-// wave share the phase, and the boundary compares happen at phase 0, where location = state).
+// SEG argument.  n and warm are whole loop bodies (P steps, a multiple of S: every g_i is one, all
+// slots of a wave share the phase, and the boundary compares happen at phase 0, where location =
+// state).
 // If every boundary holds, wave 0 traces the frame back over all segments' words (64 blocks,
 // verified chains, completeness guard) and writes the bytes; else nothing is
 // written and *done = 2 (the host decodes the frame with the batch kernel).  Input from and
