@@ -83,12 +83,18 @@ __device__ __forceinline__ int partner(int m) {
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
-// Received pair of one step: the raw bytes (hard: one symbol byte, soft: two bytes), then the
-// branch-metric operand: soft, the packed bytes for v_dot2; hard, the symbol's bit offset (8 c)
-// into the location's table of the four branch metrics (v_bfe_i32 reads offset bits 4..0 only,
-// so the symbol's bits above its two are ignored, as the reference's ignore them).  The
-// recursion converts a cycle's raw bytes only after the previous cycle's steps, so that their LDS
-// reads are waited for there and not where they are issued.
+// Hard input as staged into LDS: the symbol byte's two low bits times 8 (a byte of offsets), and
+// the same for the four bytes of a word.
+__host__ __device__ constexpr uint32_t hard_offset(uint32_t byte) { return (byte & 3u) << 3; }
+__host__ __device__ constexpr uint32_t hard_offset4(uint32_t word) { return (word & 0x03030303u) << 3; }
+
+// Received pair of one step: the staged bytes (hard: one byte, soft: two bytes), then the
+// branch-metric operand: soft, the packed bytes for v_dot2; hard, the symbol's bit offset 8 c into
+// the location's table of the four branch metrics, which the kernels store in place of the symbol
+// byte when they stage the input (hard_offset: the symbol's bits above its two are dropped, as the
+// reference's `coded & 3` drops them).  The recursion converts a cycle's bytes only after the
+// previous cycle's steps, so that their LDS reads are waited for there and not where they are
+// issued.
 template <bool SOFT>
 __device__ __forceinline__ int rx_raw(const uint8_t* p) {
     if constexpr (SOFT) {
@@ -102,7 +108,7 @@ __device__ __forceinline__ int rx_pair(int raw) {
     if constexpr (SOFT) {
         return raw;
     } else {
-        return raw << 3;
+        return raw;  // (staged as hard_offset)
     }
 }
 

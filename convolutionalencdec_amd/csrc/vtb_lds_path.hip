@@ -87,7 +87,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
             const int f = idx / in_row, off = idx - f * in_row;
             uint8_t v = 0;
             if (frame0 + f < frames && off < T * B) v = in[(frame0 + f) * in_stride + off];
-            inbuf[idx] = v;
+            inbuf[idx] = SOFT ? v : uint8_t(hard_offset(v));
         }
         __syncthreads();
     }
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void lds_path_kernel(const uin
     auto commit = [&](uint8_t* buf) {
 #pragma unroll
         for (int j = 0; j < kPf; j++)
-            if (lane + 64 * j < F * C * B) buf[lane + 64 * j] = uint8_t(pf[j]);
+            if (lane + 64 * j < F * C * B) buf[lane + 64 * j] = uint8_t(SOFT ? pf[j] : hard_offset(pf[j]));
     };
     if constexpr (GS) {
         fetch(0);
@@ -344,6 +344,7 @@ __global__ __launch_bounds__(512) void gen_seg_kernel(const uint8_t* __restrict_
         const int last = (nin - 1) & ~15;
         auto ld = [&](int o) { return *reinterpret_cast<const uint4*>(in + (o < nin ? o : last)); };
         auto stl = [&](int o, uint4 v) {
+            if (!SOFT) v = make_uint4(hard_offset4(v.x), hard_offset4(v.y), hard_offset4(v.z), hard_offset4(v.w));
             if (o < nin) *reinterpret_cast<uint4*>(sm + sg.in_lds + o) = v;
         };
         for (int base = 16 * int(threadIdx.x); base < nin; base += kGenSegStage * step) {

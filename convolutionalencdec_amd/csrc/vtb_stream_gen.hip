@@ -86,7 +86,8 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         __syncthreads();
         for (int idx = lane; idx < F * n * SB; idx += 64) {
             const int f = idx / (n * SB), o = idx - f * (n * SB);
-            sm[f * kStage * SB + o] = f0 + f < streams ? in[(f0 + f) * in_stride + size_t(c0) * SB + o] : 0;
+            const uint8_t v = f0 + f < streams ? in[(f0 + f) * in_stride + size_t(c0) * SB + o] : 0;
+            sm[f * kStage * SB + o] = SOFT ? v : uint8_t(hard_offset(v));
         }
         __syncthreads();
         const uint8_t* my = sm + fi * kStage * SB;

@@ -255,9 +255,9 @@ def sbfe8(word, offset):
 @pytest.mark.parametrize("K", [3, 4, 5, 6, 7, 8, 9])
 def test_hard_metric_table_matches_dot_form(K):
     """Hard input: the kernels read a location's branch metric from a word of four signed bytes
-    (vtb_gen_trellis.h setup_coef, rot_step: v_bfe_i32 at offset 8 c, c the raw symbol byte
-    shifted by 3, whose bits above the symbol's two fall outside the offset's five bits) instead
-    of the v_dot2 form; every symbol byte gives the dot form's value of its two low bits."""
+    (vtb_gen_trellis.h setup_coef, rot_step: v_bfe_i32 at offset 8 c, the symbol byte staged as
+    hard_offset = (byte & 3) << 3) instead of the v_dot2 form; every symbol byte gives the dot
+    form's value of its two low bits (the reference's `coded & 3`)."""
     tr = Trellis(K, CODES[K], False)
     for ph in range(tr.S):
         for l in range(tr.N):
@@ -267,4 +267,4 @@ def test_hard_metric_table_matches_dot_form(K):
                 tab |= ((s0 * (c & 1) + s1 * (c >> 1) + kap) & 0xFF) << (8 * c)
             for raw in range(256):
                 want = s0 * (raw & 1) + s1 * ((raw >> 1) & 1) + kap
-                assert sbfe8(tab, raw << 3) == want, (K, ph, l, raw)
+                assert sbfe8(tab, (raw & 3) << 3) == want, (K, ph, l, raw)
