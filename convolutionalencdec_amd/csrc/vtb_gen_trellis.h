@@ -261,9 +261,12 @@ constexpr int kTbWarm = 4 * S + 24;
 // overwrite the others' later in program order.  row(t, w) loads step t's R survivor words;
 // `base` is the frame's first bit in them; o the frame's output bytes (L bits); every lane of the
 // wave calls this (the chain checks are wave-wide).
+// traceback_span: the same over steps [t0, T) (t0 a multiple of 8) ending in location locT after
+// step T - 1, the bytes of steps t at o[(t - t0) >> 3] (the streaming decoder's emitted range,
+// vtb_stream_gen.hip); T = t0: nothing to walk.
 template <int S, int R, class Row>
-__device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned base, uint8_t* o, bool tbforce,
-                                                 uint32_t* guard_hits, Row&& row) {
+__device__ __forceinline__ void traceback_span(int t0, int T, int L, unsigned locT, int GC, unsigned base, uint8_t* o,
+                                               bool tbforce, uint32_t* guard_hits, Row&& row) {
     constexpr int kWarm = kTbWarm<S>;
     // A step's R survivor words do not depend on the walk's location (only the bit taken from them
     // does), so the walks load kTb steps' words at once and then take the kTb dependent steps
@@ -296,7 +299,7 @@ __device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned 
     auto walk_emit = [&](unsigned loc, int hi, int lo) -> unsigned {
         unsigned byte = 0;
         auto put = [&](int t) {
-            if (t < L) o[t >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
+            if (t < L) o[(t - t0) >> 3] = uint8_t(t + 8 > L ? byte & (0xffu << (t + 8 - L)) : byte);
         };
         int t = hi - 1, b = info_bit_pos<S>(hi - 1);
         for (; t >= lo && ((t + 1) & 7) != 0; t--) {
@@ -321,11 +324,11 @@ __device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned 
         }
         return loc;
     };
-    const int tbb = ((T + GC - 1) / GC + 7) / 8 * 8;
-    const int lo = bi * tbb, top = lo + tbb < T ? lo + tbb : T;
+    const int tbb = ((T - t0 + GC - 1) / GC + 7) / 8 * 8;
+    const int lo = t0 + bi * tbb, top = lo + tbb < T ? lo + tbb : T;
     const bool active = lo < T;
     const int start = top + kWarm < T ? top + kWarm : T;
-    unsigned st = active ? walk(0u, start, top) : 0u;
+    unsigned st = active ? walk(start == T ? locT : 0u, start, top) : 0u;
     unsigned s_top = st;
     if (active) st = walk_emit(st, top, lo);
     unsigned fin = st;
@@ -352,8 +355,13 @@ __device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned 
     }
     if ((unproven & cmask) && bi == 0) {
         note_guard(guard_hits);
-        walk_emit(0u, T, 0);
+        walk_emit(locT, T, t0);
     }
+}
+template <int S, int R, class Row>
+__device__ __forceinline__ void traceback_chains(int T, int L, int GC, unsigned base, uint8_t* o, bool force,
+                                                 uint32_t* guard_hits, Row&& row) {
+    traceback_span<S, R>(0, T, L, 0u, GC, base, o, force, guard_hits, row);
 }
 
 // rotate right within S bits (k in [0, S)): the location of state x after a step of phase k - 1

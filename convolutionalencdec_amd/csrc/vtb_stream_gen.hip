@@ -143,6 +143,21 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
         const uint64_t w = rg[size_t(t % W) * R + (loc >> 6)];
         return (s >> 1) | (unsigned((w >> (fi * G + lane_of<S>(loc & unsigned(G - 1)))) & 1u) << (S - 1));
     };
+    // the same from step t's R words (each word's bit taken before the select: no scratch array)
+    auto pred_w = [&](unsigned s, int t, const uint64_t (&w)[R]) -> unsigned {
+        const unsigned loc = rotr_s<S>(s, (t + 1) % S);
+        const unsigned sh = unsigned(fi * G) + lane_of<S>(loc & unsigned(G - 1));
+        unsigned x[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) x[r] = unsigned(w[r] >> sh) & 1u;
+        unsigned d = x[0];
+        if constexpr (R == 2) d = (loc & 64u) ? x[1] : x[0];
+        if constexpr (R == 4) {
+            const unsigned lo2 = (loc & 64u) ? x[1] : x[0], hi2 = (loc & 64u) ? x[3] : x[2];
+            d = (loc & 128u) ? hi2 : lo2;
+        }
+        return (s >> 1) | (d << (S - 1));
+    };
     const int e0 = st[64 * R + fi];
     const int flags = st[64 * R + 32 + fi];
     const bool lost = flags != 0 || sa.t_end - e0 > W;
@@ -161,92 +176,61 @@ __global__ __launch_bounds__(64) void gen_stream_kernel(const uint8_t* __restric
 #pragma unroll
         for (int r = 0; r < R; r++) wk[r] = unsigned(r * G + lam);
         bool walking = real && !lost && cap > e0;
-        int t = sa.t_end;
+        int t = sa.t_end, sl = t % W;  // sl: ring slot of step t
+        // the walkers' words of kMB steps loaded at once (they do not depend on the states, only
+        // the bits taken from them do), then the kMB steps one at a time with their merge checks
+        constexpr int kMB = R == 1 ? 8 : 4;
         while (__ballot(walking) != 0) {
-            if (walking) {
-                t--;
+            uint64_t w[kMB][R];
 #pragma unroll
-                for (int r = 0; r < R; r++) wk[r] = pred(wk[r], t);
-            }
-            const unsigned r0 = unsigned(__shfl(int(wk[0]), fi * G));
-            bool same = true;
+            for (int j = 0, s2 = sl; j < kMB; j++) {
+                s2 = s2 == 0 ? W - 1 : s2 - 1;
 #pragma unroll
-            for (int r = 0; r < R; r++) same = same && wk[r] == r0;
-            const bool merged = (__ballot(same) & fmask) == fmask;
-            if (walking && merged) {
-                // every survivor path passes through state r0 at step t: bits below it are final;
-                // walk on to a whole number of bytes past e0 (and below the tail cap)
-                const int lim = t < cap ? t : cap;
-                const int h = e0 + (lim - e0) / 8 * 8;
-                unsigned s0 = r0;
-                for (int u = t - 1; u >= h; u--) s0 = pred(s0, u);
-                hi = h, kloc = s0;
-                walking = false;
+                for (int r = 0; r < R; r++) w[j][r] = rg[size_t(s2) * R + r];
             }
-            if (walking && t <= e0) walking = false;
+#pragma unroll
+            for (int j = 0; j < kMB; j++) {
+                if (walking) {
+                    t--;
+                    sl = sl == 0 ? W - 1 : sl - 1;
+#pragma unroll
+                    for (int r = 0; r < R; r++) wk[r] = pred_w(wk[r], t, w[j]);
+                }
+                const unsigned r0 = unsigned(__shfl(int(wk[0]), fi * G));
+                bool same = true;
+#pragma unroll
+                for (int r = 0; r < R; r++) same = same && wk[r] == r0;
+                const bool merged = (__ballot(same) & fmask) == fmask;
+                if (walking && merged) {
+                    // every survivor path passes through state r0 at step t: bits below it are
+                    // final; walk on to a whole number of bytes past e0 (and below the tail cap)
+                    const int lim = t < cap ? t : cap;
+                    const int h = e0 + (lim - e0) / 8 * 8;
+                    unsigned s0 = r0;
+                    for (int u = t - 1; u >= h; u--) s0 = pred(s0, u);
+                    hi = h, kloc = s0;
+                    walking = false;
+                }
+                if (walking && t <= e0) walking = false;
+            }
         }
     }
     // emission of [e0, hi): the verified block-parallel traceback over the stream's G lanes
-    // (every lane runs the loops, so the cross-lane checks see the whole wave)
+    // (vtb_gen_trellis.h traceback_span, location walks with the words of several steps loaded at
+    // once; every lane calls it, so the cross-lane checks see the whole wave).  It ends in the
+    // location of state kloc after step hi - 1 (state 0 at `last`); e0 is a multiple of 8.
     const int emit_end = sa.last ? sa.t_end - S : hi;  // bits past the terminated tail are not output
     const bool emits = real && !lost && hi > e0;
-    {
-        constexpr int kWarm = 8 * S + 48;
-        const int n = hi - e0;
-        const int tbb = emits ? ((n + G - 1) / G + 7) / 8 * 8 : 8;
-        const int lo = e0 + lam * tbb, top = lo + tbb < hi ? lo + tbb : hi;
-        const bool active = emits && lo < hi;
-        const int start = top + kWarm < hi ? top + kWarm : hi;
-        unsigned s = start == hi ? kloc : 0u;
-        for (int t = start - 1; active && t >= top; t--) s = pred(s, t);
-        unsigned s_top = s;
-        for (int t = top - 1; active && t >= lo; t--) s = pred(s, t);
-        unsigned fin = s;
-        bool fixed = !active || start == hi;
-        // (chains of G blocks: at most G - 1 re-walk rounds.)  Completeness guard: a stream with
-        // a block still unproven after the cap (VTB_DEBUG bit 17: every chain with a walked block) is emitted by its
-        // lane 0 alone, walking serially from its known state at hi
-        const bool tbforce = (table.dbg & kDbgTbCap) != 0;
-        const int rounds = tbforce ? 0 : G + 1;
-        uint64_t unproven = 0;
-        for (int round = 0;; round++) {
-            const unsigned sf = unsigned(__shfl_down(int(fin), 1));  // successor block's entry state
-            const bool ok = fixed || (s_top == sf && !tbforce);
-            const uint64_t bad = ~__ballot(ok);
-            if (bad == 0) break;
-            if (round == rounds) {
-                unproven = bad;
-                break;
-            }
-            const uint64_t badf = (bad & fmask) >> (fi * G);  // this stream's failed blocks
-            if (!ok && (badf >> (lam + 1)) == 0) {
-                s = s_top = sf;
-                for (int t = top - 1; t >= lo; t--) s = pred(s, t);
-                fin = s;
-                fixed = true;
-            }
-        }
-        int elo = lo, etop = top;  // emitted steps [elo, etop), from s_top after step etop - 1
-        bool emit = active;
-        if (emits && (unproven & fmask)) {
-            emit = lam == 0, elo = e0, etop = hi, s_top = kloc;
-            if (lam == 0) note_guard(table.guard_hits);
-        }
-        if (emit) {
-            uint8_t* o = out + myf * out_stride;
-            unsigned byte = 0;
-            s = s_top;
-            for (int t = etop - 1; t >= elo; t--) {
-                byte = ((byte >> 1) | ((s & 1u) << 7)) & 0xffu;
-                const int rel = t - e0;
-                if ((rel & 7) == 0 && t < emit_end) {
-                    const int keep = emit_end - t;  // bits of this byte still inside the output
-                    o[rel >> 3] = uint8_t(keep >= 8 ? byte : byte & (0xffu << (8 - keep)));
-                }
-                s = pred(s, t);
-            }
-        }
-    }
+    // ring slot of step t in [e0, hi): t - wb, less W once past the ring's end (hi - e0 <= W)
+    const int wb = e0 - e0 % W;
+    traceback_span<S, R>(e0, emits ? hi : e0, emit_end, rotr_s<S>(kloc, hi % S), G, unsigned(fi * G),
+                         out + myf * out_stride, (table.dbg & kDbgTbCap) != 0, table.guard_hits,
+                         [&](int t, uint64_t (&w)[R]) {
+                             const int d = t - wb;
+                             const size_t slot = size_t(d >= W ? d - W : d) * R;
+#pragma unroll
+                             for (int r = 0; r < R; r++) w[r] = rg[slot + r];
+                         });
     if (real && lam == 0) {
         sa.out_bits[myf] = lost ? -1 : (sa.last ? emit_end - e0 : hi - e0);
         st[64 * R + fi] = sa.last ? 0 : (lost ? e0 : hi);

@@ -126,17 +126,18 @@ def test_every_loop_cap_covers_its_chain():
     src9 = open(os.path.join(CSRC, "vtb_k9.hip")).read()
     assert "const int per = (Tq + 31) / 32;" in src9 and "const int per = (Tq + 63) / 64;" in src9
     assert _caps("vtb_genk.hip") == ["65"]  # one chain over the 64 lanes
-    # generic batch and single-frame kernels share traceback_chains: GC lanes (blocks) per chain,
-    # GC = G (lds_path_kernel) or 64 (gen_seg_kernel)
+    # generic batch, single-frame and stream kernels share traceback_span: GC lanes (blocks) per
+    # chain, GC = G (lds_path_kernel, gen_stream_kernel: one stream's lanes) or 64 (gen_seg_kernel)
     assert _caps("vtb_gen_trellis.h") == ["GC + 1"]
     assert _caps("vtb_lds_path.hip") == []
     src = open(os.path.join(CSRC, "vtb_lds_path.hip")).read()
     assert src.count("traceback_chains<S, R>(T, L, G,") == 1 and src.count("traceback_chains<S, R>(T, L, 64,") == 1
-    assert _caps("vtb_stream_gen.hip") == ["G + 1"]
+    assert _caps("vtb_stream_gen.hip") == []
+    src = open(os.path.join(CSRC, "vtb_stream_gen.hip")).read()
+    assert src.count("traceback_span<S, R>(e0, emits ? hi : e0, emit_end, rotr_s<S>(kloc, hi % S), G,") == 1
 
 
-@pytest.mark.parametrize("fname", ["vtb_k7_lds.hip", "vtb_k9.hip", "vtb_genk.hip", "vtb_gen_trellis.h",
-                                   "vtb_stream_gen.hip"])
+@pytest.mark.parametrize("fname", ["vtb_k7_lds.hip", "vtb_k9.hip", "vtb_genk.hip", "vtb_gen_trellis.h"])
 def test_every_guard_has_a_slow_path(fname):
     """After each loop an unproven chain reaches an exact slow path, and the testing counter
     notes it (note_guard)."""
